@@ -1,0 +1,226 @@
+"""bench.py -- map-phase chunks/s of the MI355X engine (BASELINE.json metric).
+
+A "step" = one map phase over one batch: every GPU takes its chunks_per_gpu synthetic
+2048-token chunks (the workload of BASELINE.json configs[1]: one 16k-token doc split
+into 8 chunks), prefills them packed, decodes exactly 256 greedy tokens each
+(ignore_eos), and the per-chunk summary ids are gathered to rank 0
+over RCCL.  value = chunks of all ranks / max-over-ranks wall time.  N > 1 is weak
+scaling: each rank owns its own document's chunks.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "map-reduced-approach-for-vietnamese-long-document-summarization_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "map-phase chunks/sec (2k-tok chunk, 256-tok summary) at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA
+
+
+def synthetic_chunks(n, prompt_len, doc, vocab, bos, seed=0):
+    """Token ids of n chunks: BOS + Llama-3 header ids + uniform body over [0, 128000)
+    (no tokenizer / dataset offline; timing of dense ops does not depend on values)."""
+    head = [bos, 128006, 9125, 128007, 271, 128009, 128006, 882, 128007, 271]
+    rng = np.random.default_rng(seed + 1000 * doc)
+    tail = [128009, 128006, 78191, 128007, 271]
+    out = []
+    for _ in range(n):
+        body = rng.integers(0, min(128000, vocab), size=prompt_len - len(head) - len(tail))
+        ids = np.array(head + body.tolist() + tail, np.int32)
+        out.append(np.clip(ids, 0, vocab - 1))
+    return out
+
+
+def gemv_bytes_per_step(cfg, B):
+    """Algorithmic HBM bytes of one decode step's layer projections: every weight matrix
+    once + the B activation rows in/out (SURVEY.md §8d weight term, without lm_head)."""
+    H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
+    qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
+    w = 2 * (qkv * H + H * cfg.n_heads * D + 2 * F * H + H * F)
+    act = 2 * B * (H + qkv + cfg.n_heads * D + H + H + F + F + H) + 4 * B * H * 4
+    return cfg.n_layers * (w + act)
+
+
+def prefill_flops_per_chunk(cfg, P):
+    """2*params_linear*P + lm_head on the last token + causal attention."""
+    H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
+    lin = cfg.n_layers * ((cfg.n_heads + 2 * cfg.n_kv_heads) * D * H + H * cfg.n_heads * D + 3 * H * F)
+    attn = cfg.n_layers * cfg.n_heads * 4 * D * (P * (P + 1) // 2)
+    return 2 * lin * P + 2 * cfg.vocab * H + attn
+
+
+def cpu_baseline(cfg, prompt_len, gen_len, decode_sample=16):
+    """Oracle (numpy, CPU) on a bounded sample of the same workload, scaled to one chunk:
+    one full-width layer prefilled over a prompt_len chunk + decode_sample cached decode
+    steps through that layer + the tied lm_head, times n_layers / gen_len."""
+    from oracle.llama_ref import OracleLlama
+    one = cfg.with_(n_layers=1)
+    rng = np.random.default_rng(0)
+    H, D = cfg.hidden, cfg.head_dim
+
+    def lin(r, c):
+        return (rng.standard_normal((r, c), dtype=np.float32) * 0.02)
+
+    w = {"embed": lin(cfg.vocab, H), "final_norm": np.ones(H, np.float32),
+         "layers": [{"attn_norm": np.ones(H, np.float32), "ffn_norm": np.ones(H, np.float32),
+                     "wq": lin(cfg.n_heads * D, H), "wk": lin(cfg.n_kv_heads * D, H),
+                     "wv": lin(cfg.n_kv_heads * D, H), "wo": lin(H, cfg.n_heads * D),
+                     "w_gate": lin(cfg.ffn, H), "w_up": lin(cfg.ffn, H), "w_down": lin(H, cfg.ffn)}]}
+    w["lm_head"] = w["embed"]
+    o = OracleLlama(one, w)
+    ids = rng.integers(0, 128000, size=prompt_len)
+    cache = o.new_cache()
+    t0 = time.perf_counter()
+    logits, _ = o.forward(ids, cache)
+    t_pre = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for _ in range(decode_sample):
+        logits, _ = o.forward([int(np.argmax(logits))], cache)
+    t_dec = (time.perf_counter() - t0) / decode_sample
+    # lm_head is paid once per token, the layer n_layers times
+    t0 = time.perf_counter()
+    for _ in range(4):
+        _ = w["embed"] @ np.ones(H, np.float32)
+    t_head = (time.perf_counter() - t0) / 4
+    t_layer_dec = max(t_dec - t_head, 1e-9)
+    t_layer_pre = max(t_pre - t_head, 1e-9)
+    chunk_s = cfg.n_layers * t_layer_pre + t_head + (gen_len - 1) * (cfg.n_layers * t_layer_dec + t_head)
+    try:
+        import threadpoolctl
+        cores = max(p["num_threads"] for p in threadpoolctl.threadpool_info()) if threadpoolctl.threadpool_info() else 1
+    except Exception:
+        cores = os.cpu_count() or 1
+    return {"value": 1.0 / chunk_s, "unit": "chunks/s", "cores": int(cores), "kind": "port",
+            "sample": (f"numpy oracle, Llama-3.2-3B width, 1 of {cfg.n_layers} layers: {prompt_len}-tok "
+                       f"prefill ({t_pre:.2f}s) + {decode_sample} cached decode steps "
+                       f"({t_dec * 1e3:.1f} ms/step incl. lm_head {t_head * 1e3:.1f} ms), "
+                       f"scaled to {cfg.n_layers} layers x {gen_len} tokens")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--chunks-per-gpu", type=int, default=8)
+    ap.add_argument("--prompt-len", type=int, default=2048)
+    ap.add_argument("--gen-len", type=int, default=256)
+    ap.add_argument("--model", default="llama3.2-3b")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true", help="skip HIP-event timing of the GEMV class")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from mapsum import _lib as L
+    from mapsum.config import CONFIGS
+    from mapsum.dist import Unit, env_rank, gather_summaries, pack_results
+    from mapsum.engine import Engine
+
+    cfg = CONFIGS[args.model]
+    rank, local_rank, world = env_rank()
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    B = args.chunks_per_gpu
+    max_ctx = args.prompt_len + args.gen_len
+    eng = Engine(cfg, device=local_rank, max_batch=B, max_ctx=max_ctx,
+                 max_prefill_tokens=B * args.prompt_len)
+    eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
+    chunks = synthetic_chunks(B, args.prompt_len, doc=rank, vocab=cfg.vocab, bos=cfg.bos_id)
+    units = [Unit(rank, i, args.prompt_len) for i in range(B)]
+
+    def one_step():
+        res = eng.generate(chunks, num_predict=args.gen_len, ignore_eos=True)
+        packed = pack_results(units, [r.ids for r in res], args.gen_len)
+        return gather_summaries(packed, B, device=dev)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        one_step()
+    if not args.no_roofline:
+        eng.set_profiling(1 << L.K_GEMV)
+    eng.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rows = one_step()
+    barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.stats()
+    total_chunks = world * B * args.steps
+    value = total_chunks / dt
+    assert rows is not None and len(rows) == world * B
+
+    roof = None
+    if not args.no_roofline and st["kernel_launches"][L.K_GEMV] > 0:
+        steps_dec = st["decode_steps"]
+        gemv_s = st["kernel_ms"][L.K_GEMV] / 1e3
+        launches = st["kernel_launches"][L.K_GEMV]
+        bytes_total = gemv_bytes_per_step(cfg, B) * steps_dec
+        ach = bytes_total / gemv_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": "gemv_kernel (decode QKV/O/gate-up/down projections)",
+                "bytes_per_launch": int(bytes_total / launches),
+                "avg_launch_us": round(gemv_s / launches * 1e6, 2)}
+    pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * B * args.steps
+    out = {
+        "metric": METRIC, "value": round(value, 4), "unit": "chunks/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "data": "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)",
+        "config": {"workload": f"configs[1]: {B} x {args.prompt_len}-tok chunks -> {args.gen_len}-tok "
+                               f"greedy summaries per GPU (ignore_eos), batched prefill + decode, "
+                               f"summary ids gathered to rank 0",
+                   "model": cfg.name, "chunks_per_gpu": B, "prompt_tokens": args.prompt_len,
+                   "summary_tokens": args.gen_len, "global_batch": world * B,
+                   "seq_len": args.prompt_len + args.gen_len, "parallelism": f"chunk-dp{world}"},
+        "breakdown": {"prefill_ms_per_step": round(st["prefill_ms"] / args.steps, 2),
+                      "decode_ms_per_step": round(st["decode_ms"] / args.steps, 2),
+                      "decode_steps": st["decode_steps"],
+                      "prefill_tflops": round(pre_flops / (st["prefill_ms"] / 1e3) / 1e12, 1)
+                      if st["prefill_ms"] else None,
+                      "gemv_ms_total": round(st["kernel_ms"][L.K_GEMV], 2)},
+        "roofline": roof,
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, args.prompt_len, args.gen_len)
+    eng.close()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * mapsum.h -- C-ABI of libmapsum.so, the MI355X-native map-phase engine.
+ *
+ * What this replaces.  The reference has no native boundary: its
+ * map call is one HTTP request per chunk,
+ *     OllamaLLM._call(prompt) -> requests.post(f"{url}/api/generate",
+ *         json={"model", "prompt", "stream": False, "options": {"num_predict": N}})
+ *         -> resp.json()["response"]
+ * (run_full_evaluation_pipeline.py:80-106; runner copies
+ *  runners/run_summarization_ollama_mapreduce.py:37-49,
+ *  runners/run_summarization_ollama_mapreduce_critique.py:63-79,
+ *  runners/run_summarization_ollama_mapreduce_hierarchical.py:56-68).
+ * Everything behind that request (template -> tokenize -> prefill -> decode ->
+ * detokenize) happens inside Ollama.  libmapsum takes over the
+ * prefill/decode part on ids: the Python host (mapsum/compat.py OllamaLLM) keeps
+ * the prompt-in/summary-out contract and calls
+ *     ms_submit (one per chunk)  ~ the body of one /api/generate request
+ *     ms_step                    ~ one scheduler iteration (admit+prefill, decode)
+ *     ms_poll                    ~ resp.json()["response"] (as ids)
+ * Errors: every entry point returns an int status (0 = OK, < 0 errno-like) and
+ * never throws across the ABI; ms_last_error() gives the text.  The Python
+ * wrapper raises RuntimeError, mirroring resp.raise_for_status()
+ * (run_full_evaluation_pipeline.py:91).
+ * Ownership: input ids are copied at submit; result id buffers are owned by the
+ * engine and stay valid until the next ms_poll / ms_destroy.  One engine per GPU
+ * per process; an engine is not thread-safe.
+ */
+#ifndef MAPSUM_H
+#define MAPSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MS_ABI_VERSION 1
+
+/* status codes */
+#define MS_OK 0
+#define MS_EIO -5       /* device / runtime failure                  */
+#define MS_ENOMEM -12   /* device allocation failed                  */
+#define MS_EBUSY -16    /* operation not allowed while work pending  */
+#define MS_EINVAL -22   /* bad argument                              */
+#define MS_ENOSPC -28   /* request can never fit (ctx / KV pages)    */
+
+/* finish reasons (ms_result.finish_reason) -- Ollama's done_reason "stop"/"length" */
+#define MS_FINISH_EOS 1
+#define MS_FINISH_LENGTH 2
+#define MS_FINISH_ERROR 3
+
+/* ms_submit flags */
+#define MS_FLAG_IGNORE_EOS 1u /* bench mode: always generate num_predict tokens */
+
+/* logical weight tensors for ms_load_weight ([rows][cols] row-major bf16, HF
+ * nn.Linear layout [out][in]); the engine fuses Q|K|V and interleaves gate/up
+ * on upload. */
+enum ms_tensor {
+  MS_T_EMBED = 0,      /* [vocab][hidden]          */
+  MS_T_ATTN_NORM = 1,  /* [hidden]                 */
+  MS_T_WQ = 2,         /* [n_heads*head_dim][hidden] */
+  MS_T_WK = 3,         /* [n_kv*head_dim][hidden]  */
+  MS_T_WV = 4,         /* [n_kv*head_dim][hidden]  */
+  MS_T_WO = 5,         /* [hidden][n_heads*head_dim] */
+  MS_T_FFN_NORM = 6,   /* [hidden]                 */
+  MS_T_WGATE = 7,      /* [ffn][hidden]            */
+  MS_T_WUP = 8,        /* [ffn][hidden]            */
+  MS_T_WDOWN = 9,      /* [hidden][ffn]            */
+  MS_T_FINAL_NORM = 10,/* [hidden]                 */
+  MS_T_LM_HEAD = 11    /* [vocab][hidden]; only when tie_embeddings == 0 */
+};
+
+typedef struct ms_config {
+  int32_t abi_version;          /* = MS_ABI_VERSION */
+  /* model (Llama-3.2 family; head_dim must be 128) */
+  int32_t n_layers, hidden, n_heads, n_kv_heads, head_dim, ffn, vocab;
+  float rope_theta, rope_factor, rope_low_freq_factor, rope_high_freq_factor;
+  int32_t rope_orig_ctx;
+  float norm_eps;
+  int32_t tie_embeddings;
+  /* engine */
+  int32_t device;               /* HIP device ordinal                         */
+  int32_t max_batch;            /* sequences in flight (<= 256)               */
+  int32_t max_ctx;              /* prompt + generated tokens per sequence     */
+  int32_t max_prefill_tokens;   /* packed prompt tokens per prefill pass      */
+  int32_t n_pages;              /* KV pages of 64 tokens; 0 = enough for all  */
+  int32_t n_eos;                /* end-of-turn ids (<|eot_id|> etc.)          */
+  int32_t eos_ids[8];
+} ms_config;
+
+typedef struct ms_result {
+  uint64_t tag;          /* the caller's tag from ms_submit                    */
+  const int32_t* ids;    /* generated ids (EOS excluded); engine-owned          */
+  int32_t n_ids;
+  int32_t finish_reason; /* MS_FINISH_*                                         */
+  int32_t n_prompt;
+  int32_t _pad;
+} ms_result;
+
+typedef struct ms_stats {
+  int64_t prefill_tokens;     /* prompt tokens processed                       */
+  int64_t decode_tokens;      /* tokens produced by decode steps               */
+  int64_t prefill_passes, decode_steps;
+  int64_t finished;
+  double prefill_ms, decode_ms; /* device time (events) when profiling is on   */
+  double kernel_ms[8];          /* per kernel class, when profiling is on:
+                                   0 gemm(prefill) 1 attn_prefill 2 gemv(decode)
+                                   3 attn_decode 4 lm_head 5 norm/rope/misc     */
+  int64_t kernel_launches[8];
+} ms_stats;
+
+typedef struct ms_engine ms_engine;
+
+/* ---- engine lifecycle ------------------------------------------------------ */
+int ms_create(const ms_config* cfg, ms_engine** out);
+int ms_destroy(ms_engine* e);
+/* e == NULL returns the last error of a failed ms_create / op call */
+const char* ms_last_error(const ms_engine* e);
+
+/* ---- weights ---------------------------------------------------------------- */
+int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host_bf16,
+                   int64_t n_elems);
+/* device-side counter-based N(0,std)-like init; restated in oracle/synth.py */
+int ms_init_synthetic(ms_engine* e, uint64_t seed, float std, float norm_jitter);
+
+/* ---- request path (replaces one /api/generate per chunk) -------------------- */
+int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict,
+              uint32_t flags, uint64_t tag);
+/* one scheduler iteration; returns sequences still waiting or running (>= 0) */
+int ms_step(ms_engine* e);
+/* copies up to cap finished results; returns the number copied */
+int ms_poll(ms_engine* e, ms_result* out, int32_t cap);
+int ms_pending(const ms_engine* e);
+int ms_get_stats(const ms_engine* e, ms_stats* out);
+int ms_reset_stats(ms_engine* e);
+/* bit mask of kernel classes to bracket with HIP events (0 = off) */
+int ms_set_profiling(ms_engine* e, uint32_t class_mask);
+int ms_synchronize(ms_engine* e);
+
+/* ---- parity probe (tests): one prompt through the prefill path -------------- */
+/* hidden_out: [n][hidden] fp32 residual after `n_layers_run` layers (or NULL);
+   logits_out: [n][vocab] fp32 logits of every position (or NULL; needs
+   n_layers_run == n_layers). */
+int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run,
+               float* hidden_out, float* logits_out);
+
+/* ---- op-level entry points (device pointers; stream = hipStream_t or NULL) -- */
+#define MS_EPI_STORE_BF16 0  /* out bf16 [M][ldo]                              */
+#define MS_EPI_ADD_F32 1     /* out fp32 [M][ldo] += acc  (residual add)       */
+#define MS_EPI_SWIGLU 2      /* W rows interleaved gate/up per 16; out bf16 [M][N/2] */
+#define MS_EPI_STORE_F32 3   /* out fp32 [M][ldo]                              */
+/* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0 */
+int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+               int32_t ldo, int32_t epilogue, void* stream);
+/* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
+int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
+int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+               int32_t ldo, int32_t epilogue, void* workspace, void* stream);
+/* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
+int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
+                  const int32_t* row_idx, void* stream);
+/* ids[r] = argmax_j logits[r][j] (ties -> lowest j) */
+int ms_op_argmax(const void* logits, int32_t rows, int32_t n, int32_t* ids, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAPSUM_H */

@@ -1,0 +1,859 @@
+// engine.cpp -- libmapsum: the map-phase engine behind the C-ABI of include/mapsum.h.
+//
+// One engine = one GPU = one process.  It replaces, for every chunk the map node
+// sends (runners/run_summarization_ollama_mapreduce.py:103-106 ->
+// run_full_evaluation_pipeline.py:80-106 -> POST /api/generate), what Ollama does
+// with the prompt ids: prefill, greedy decode until an end-of-turn id or
+// num_predict.  Unlike the reference, whose blocking
+// _acall (run_full_evaluation_pipeline.py:108-109) serialises the map fan-out,
+// every submitted chunk joins one continuous batch:
+//   ms_step = admit waiting chunks (slot + KV pages reserved for prompt+num_predict)
+//             -> one packed varlen prefill pass over all admitted prompts
+//             -> one decode step for every running sequence.
+// Device memory is laid out once at ms_create for the configured max batch:
+// bf16 weights (Q|K|V fused, gate/up interleaved per 16 rows), a paged bf16 KV
+// pool [layer][page][kv_head][64][128], fp32 residual stream, bf16 activations.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "mapsum.h"
+
+using namespace ms;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct MsError : std::runtime_error {
+  int code;
+  MsError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_OK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      throw MsError(MS_EIO, std::string(#expr) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+#define REQUIRE(cond, code, msg)                      \
+  do {                                                \
+    if (!(cond)) throw MsError((code), (msg));        \
+  } while (0)
+
+enum KClass { K_GEMM = 0, K_ATTN_PREFILL = 1, K_GEMV = 2, K_ATTN_DECODE = 3, K_LMHEAD = 4, K_MISC = 5 };
+
+struct Seq {
+  uint64_t tag = 0;
+  std::vector<int32_t> prompt;
+  int32_t num_predict = 0;
+  uint32_t flags = 0;
+  int slot = -1;
+  int len = 0;  // tokens whose K/V are in the cache
+  std::vector<int32_t> out;
+  std::vector<int32_t> pages;
+  int finish = 0;
+};
+
+struct Layer {
+  bf16_t *attn_norm = nullptr, *wqkv = nullptr, *wo = nullptr, *ffn_norm = nullptr,
+         *wgu = nullptr, *wdown = nullptr;
+};
+
+}  // namespace
+
+struct ms_engine {
+  ms_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  int H = 0, Hq = 0, Hk = 0, D = 128, F = 0, V = 0, L = 0, QKVN = 0;
+  int max_pages = 0, n_pages = 0, Tmax = 0;
+  std::vector<void*> allocs;
+  std::vector<Layer> layers;
+  bf16_t *embed = nullptr, *final_norm = nullptr, *lm_head = nullptr;
+  float *cos_tab = nullptr, *sin_tab = nullptr;
+  bf16_t *kpool = nullptr, *vpool = nullptr;
+  size_t layer_kv_elems = 0;
+  int32_t* bt_d = nullptr;
+  std::vector<int32_t> bt_h;
+  std::vector<int> free_pages, free_slots;
+  float* x = nullptr;
+  bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
+  float* logits = nullptr;
+  int32_t* ids_out_d = nullptr;
+  void* gemv_ws = nullptr;
+  float* attn_ws = nullptr;
+  int32_t* args_d = nullptr;
+  int32_t* args_h = nullptr;  // pinned
+  size_t args_cap = 0;
+  std::deque<std::unique_ptr<Seq>> waiting;
+  std::vector<std::unique_ptr<Seq>> running;
+  std::vector<std::unique_ptr<Seq>> done, polled;
+  ms_stats stats{};
+  uint32_t prof_mask = 0;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_pending;  // (class, start event index); end = start+1
+  size_t ev_used = 0;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+
+  template <class T>
+  T* dalloc(size_t n, bool zero = false) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e != hipSuccess)
+      throw MsError(MS_ENOMEM, "hipMalloc(" + std::to_string(n * sizeof(T)) + " B) failed: " +
+                                   hipGetErrorString(e));
+    allocs.push_back(p);
+    if (zero) HIP_OK(hipMemset(p, 0, n * sizeof(T)));
+    return (T*)p;
+  }
+
+  // ---- profiling brackets -------------------------------------------------
+  void prof_begin(int cls) {
+    if (!((prof_mask >> cls) & 1)) return;
+    if (ev_used + 2 > ev_pool.size()) {
+      for (int i = 0; i < 64; ++i) {
+        hipEvent_t ev;
+        HIP_OK(hipEventCreate(&ev));
+        ev_pool.push_back(ev);
+      }
+    }
+    ev_pending.push_back({cls, (int)ev_used});
+    HIP_OK(hipEventRecord(ev_pool[ev_used], stream));
+    ev_used += 2;
+  }
+  void prof_end(int cls) {
+    if (!((prof_mask >> cls) & 1)) return;
+    HIP_OK(hipEventRecord(ev_pool[ev_pending.back().second + 1], stream));
+  }
+  void prof_collect() {  // after a stream sync
+    for (auto& pr : ev_pending) {
+      float ms_ = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms_, ev_pool[pr.second], ev_pool[pr.second + 1]));
+      stats.kernel_ms[pr.first] += ms_;
+      stats.kernel_launches[pr.first] += 1;
+    }
+    ev_pending.clear();
+    ev_used = 0;
+  }
+
+  KVView kv_layer(int l) const {
+    KVView v;
+    v.k = kpool + (size_t)l * layer_kv_elems;
+    v.v = vpool + (size_t)l * layer_kv_elems;
+    v.block_table = bt_d;
+    v.max_pages = max_pages;
+    v.n_kv_heads = Hk;
+    return v;
+  }
+
+  void gemm_or_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                    int epi, bool decode, int cls) {
+    prof_begin(cls);
+    if (decode && M <= 64)
+      launch_gemv(X, W, out, M, N, K, ldo, epi, gemv_ws, stream);
+    else
+      launch_gemm(X, W, out, M, N, K, ldo, epi, stream);
+    prof_end(cls);
+  }
+
+  // one transformer layer over T packed tokens (decode: T = B rows, one token each)
+  void run_layer(int l, int T, bool decode, const int32_t* tok_pos, const int32_t* tok_slot,
+                 const PrefillAttnArgs& pa, const DecodeAttnArgs& da) {
+    const Layer& Ly = layers[l];
+    const int kc = decode ? K_GEMV : K_GEMM;
+    prof_begin(K_MISC);
+    launch_rmsnorm(x, Ly.attn_norm, xb, T, H, cfg.norm_eps, nullptr, stream);
+    prof_end(K_MISC);
+    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_BF16, decode, kc);
+    KVView kv = kv_layer(l);
+    prof_begin(K_MISC);
+    launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
+    prof_end(K_MISC);
+    if (decode) {
+      prof_begin(K_ATTN_DECODE);
+      launch_attn_decode(qkv, attn, Hq, Hk, kv, da, attn_ws, stream);
+      prof_end(K_ATTN_DECODE);
+    } else {
+      prof_begin(K_ATTN_PREFILL);
+      launch_attn_prefill(qkv, attn, Hq, Hk, kv, pa, stream);
+      prof_end(K_ATTN_PREFILL);
+    }
+    gemm_or_gemv(attn, Ly.wo, x, T, H, Hq * D, H, MS_EPI_ADD_F32, decode, kc);
+    prof_begin(K_MISC);
+    launch_rmsnorm(x, Ly.ffn_norm, xb, T, H, cfg.norm_eps, nullptr, stream);
+    prof_end(K_MISC);
+    gemm_or_gemv(xb, Ly.wgu, hbuf, T, 2 * F, H, F, MS_EPI_SWIGLU, decode, kc);
+    gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
+  }
+
+  int32_t* upload_args(const std::vector<int32_t>& a) {
+    REQUIRE(a.size() <= args_cap, MS_EINVAL, "step arguments exceed the staging buffer");
+    std::memcpy(args_h, a.data(), a.size() * sizeof(int32_t));
+    HIP_OK(hipMemcpyAsync(args_d, args_h, a.size() * sizeof(int32_t), hipMemcpyHostToDevice, stream));
+    return args_d;
+  }
+};
+
+namespace {
+
+int fail(ms_engine* e, const MsError& x) {
+  if (e) e->err = x.what();
+  g_last_error = x.what();
+  return x.code;
+}
+
+template <class Fn>
+int guarded(ms_engine* e, Fn&& fn) {
+  try {
+    return fn();
+  } catch (const MsError& x) {
+    return fail(e, x);
+  } catch (const std::exception& x) {
+    return fail(e, MsError(MS_EIO, x.what()));
+  } catch (...) {
+    return fail(e, MsError(MS_EIO, "unknown exception"));
+  }
+}
+
+// llama3-scaled rotate-half tables (oracle/llama_ref.py rope_inv_freq restates this)
+void rope_tables(const ms_config& c, int max_ctx, std::vector<float>& cs, std::vector<float>& sn) {
+  const int half = c.head_dim / 2;
+  std::vector<double> inv(half);
+  for (int i = 0; i < half; ++i) {
+    double f = 1.0 / std::pow((double)c.rope_theta, (2.0 * i) / c.head_dim);
+    if (c.rope_factor > 0) {
+      const double low_wl = c.rope_orig_ctx / (double)c.rope_low_freq_factor;
+      const double high_wl = c.rope_orig_ctx / (double)c.rope_high_freq_factor;
+      const double wl = 2.0 * M_PI / f;
+      double out = wl > low_wl ? f / c.rope_factor : f;
+      if (!(wl < high_wl) && !(wl > low_wl)) {
+        const double smooth = (c.rope_orig_ctx / wl - c.rope_low_freq_factor) /
+                              (c.rope_high_freq_factor - c.rope_low_freq_factor);
+        out = (1.0 - smooth) * out / c.rope_factor + smooth * out;
+      }
+      f = out;
+    }
+    inv[i] = f;
+  }
+  cs.resize((size_t)max_ctx * half);
+  sn.resize((size_t)max_ctx * half);
+  for (int p = 0; p < max_ctx; ++p)
+    for (int i = 0; i < half; ++i) {
+      const double a = (double)p * inv[i];
+      cs[(size_t)p * half + i] = (float)std::cos(a);
+      sn[(size_t)p * half + i] = (float)std::sin(a);
+    }
+}
+
+void validate_config(const ms_config& c) {
+  REQUIRE(c.abi_version == MS_ABI_VERSION, MS_EINVAL, "abi_version mismatch");
+  REQUIRE(c.head_dim == 128, MS_EINVAL, "head_dim must be 128");
+  REQUIRE(c.n_layers > 0 && c.n_heads > 0 && c.n_kv_heads > 0 && c.n_heads % c.n_kv_heads == 0,
+          MS_EINVAL, "bad head/layer counts");
+  REQUIRE(c.n_heads / c.n_kv_heads <= 16, MS_EINVAL, "GQA group must be <= 16");
+  REQUIRE(c.hidden == c.n_heads * c.head_dim, MS_EINVAL, "hidden must equal n_heads*head_dim");
+  REQUIRE(c.hidden % 256 == 0 && c.ffn % 256 == 0, MS_EINVAL, "hidden and ffn must be multiples of 256");
+  REQUIRE(c.vocab % 16 == 0 && c.vocab > 0, MS_EINVAL, "vocab must be a multiple of 16");
+  REQUIRE(c.max_batch >= 1 && c.max_batch <= 256, MS_EINVAL, "max_batch must be in [1,256]");
+  REQUIRE(c.max_ctx >= 64 && c.max_ctx <= 131072, MS_EINVAL, "max_ctx must be in [64,131072]");
+  REQUIRE(c.max_prefill_tokens >= 1, MS_EINVAL, "max_prefill_tokens must be >= 1");
+  REQUIRE(c.n_eos >= 0 && c.n_eos <= 8, MS_EINVAL, "n_eos must be in [0,8]");
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+int ms_create(const ms_config* cfg, ms_engine** out) {
+  if (!cfg || !out) {
+    g_last_error = "ms_create: null argument";
+    return MS_EINVAL;
+  }
+  *out = nullptr;
+  auto e = std::make_unique<ms_engine>();
+  int rc = guarded(nullptr, [&]() -> int {
+    validate_config(*cfg);
+    ms_engine& E = *e;
+    E.cfg = *cfg;
+    HIP_OK(hipSetDevice(cfg->device));
+    HIP_OK(hipStreamCreateWithFlags(&E.stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreate(&E.ev_a));
+    HIP_OK(hipEventCreate(&E.ev_b));
+    E.H = cfg->hidden; E.Hq = cfg->n_heads; E.Hk = cfg->n_kv_heads; E.D = cfg->head_dim;
+    E.F = cfg->ffn; E.V = cfg->vocab; E.L = cfg->n_layers;
+    E.QKVN = (E.Hq + 2 * E.Hk) * E.D;
+    E.max_pages = (cfg->max_ctx + kPage - 1) / kPage;
+    E.n_pages = cfg->n_pages > 0 ? cfg->n_pages : cfg->max_batch * E.max_pages;
+    E.Tmax = std::max(cfg->max_prefill_tokens, cfg->max_batch);
+    // weights
+    E.embed = E.dalloc<bf16_t>((size_t)E.V * E.H);
+    E.lm_head = cfg->tie_embeddings ? E.embed : E.dalloc<bf16_t>((size_t)E.V * E.H);
+    E.final_norm = E.dalloc<bf16_t>(E.H);
+    E.layers.resize(E.L);
+    for (auto& Ly : E.layers) {
+      Ly.attn_norm = E.dalloc<bf16_t>(E.H);
+      Ly.ffn_norm = E.dalloc<bf16_t>(E.H);
+      Ly.wqkv = E.dalloc<bf16_t>((size_t)E.QKVN * E.H);
+      Ly.wo = E.dalloc<bf16_t>((size_t)E.H * E.Hq * E.D);
+      Ly.wgu = E.dalloc<bf16_t>((size_t)2 * E.F * E.H);
+      Ly.wdown = E.dalloc<bf16_t>((size_t)E.H * E.F);
+    }
+    // rope tables
+    std::vector<float> cs, sn;
+    rope_tables(*cfg, cfg->max_ctx, cs, sn);
+    E.cos_tab = E.dalloc<float>(cs.size());
+    E.sin_tab = E.dalloc<float>(sn.size());
+    HIP_OK(hipMemcpy(E.cos_tab, cs.data(), cs.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(E.sin_tab, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
+    // paged KV pool (zeroed: stale-page bytes are always finite)
+    E.layer_kv_elems = (size_t)E.n_pages * E.Hk * kPage * E.D;
+    E.kpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
+    E.vpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
+    E.bt_h.assign((size_t)cfg->max_batch * E.max_pages, 0);
+    E.bt_d = E.dalloc<int32_t>(E.bt_h.size(), true);
+    for (int p = E.n_pages - 1; p >= 0; --p) E.free_pages.push_back(p);
+    for (int s = cfg->max_batch - 1; s >= 0; --s) E.free_slots.push_back(s);
+    // activations
+    const size_t T = E.Tmax;
+    E.x = E.dalloc<float>(T * E.H);
+    E.xb = E.dalloc<bf16_t>(T * E.H);
+    E.qkv = E.dalloc<bf16_t>(T * E.QKVN);
+    E.attn = E.dalloc<bf16_t>(T * E.Hq * E.D);
+    E.hbuf = E.dalloc<bf16_t>(T * E.F);
+    E.logits = E.dalloc<float>((size_t)cfg->max_batch * E.V);
+    E.ids_out_d = E.dalloc<int32_t>(cfg->max_batch);
+    const int Md = std::min(cfg->max_batch, 64);
+    size_t gws = 0;
+    const int shapes[5][2] = {{E.QKVN, E.H}, {E.H, E.Hq * E.D}, {2 * E.F, E.H}, {E.H, E.F}, {E.V, E.H}};
+    for (auto& sh : shapes) gws = std::max(gws, gemv_workspace_bytes(Md, sh[0], sh[1]));
+    E.gemv_ws = E.dalloc<char>(gws, true);
+    E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx));
+    E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
+    E.args_d = E.dalloc<int32_t>(E.args_cap);
+    HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
+    HIP_OK(hipDeviceSynchronize());
+    return MS_OK;
+  });
+  if (rc != MS_OK) {
+    ms_destroy(e.release());
+    return rc;
+  }
+  *out = e.release();
+  return MS_OK;
+}
+
+int ms_destroy(ms_engine* e) {
+  if (!e) return MS_OK;
+  (void)hipSetDevice(e->cfg.device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (void* p : e->allocs) (void)hipFree(p);
+  if (e->args_h) (void)hipHostFree(e->args_h);
+  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  if (e->ev_a) (void)hipEventDestroy(e->ev_a);
+  if (e->ev_b) (void)hipEventDestroy(e->ev_b);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+  return MS_OK;
+}
+
+const char* ms_last_error(const ms_engine* e) {
+  if (e) return e->err.c_str();
+  return g_last_error.c_str();
+}
+
+int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host, int64_t n) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(host != nullptr, MS_EINVAL, "null weight buffer");
+    HIP_OK(hipSetDevice(E.cfg.device));
+    const bool per_layer = tensor != MS_T_EMBED && tensor != MS_T_FINAL_NORM && tensor != MS_T_LM_HEAD;
+    REQUIRE(!per_layer || (layer >= 0 && layer < E.L), MS_EINVAL, "layer out of range");
+    bf16_t* dst = nullptr;
+    int rows = 0, cols = 0, mul = 16, add = 0;
+    const int H = E.H, QD = E.Hq * E.D, KD = E.Hk * E.D;
+    switch (tensor) {
+      case MS_T_EMBED: dst = E.embed; rows = E.V; cols = H; break;
+      case MS_T_LM_HEAD:
+        REQUIRE(!E.cfg.tie_embeddings, MS_EINVAL, "lm_head is tied to the embedding");
+        dst = E.lm_head; rows = E.V; cols = H; break;
+      case MS_T_FINAL_NORM: dst = E.final_norm; rows = 1; cols = H; break;
+      case MS_T_ATTN_NORM: dst = E.layers[layer].attn_norm; rows = 1; cols = H; break;
+      case MS_T_FFN_NORM: dst = E.layers[layer].ffn_norm; rows = 1; cols = H; break;
+      case MS_T_WQ: dst = E.layers[layer].wqkv; rows = QD; cols = H; break;
+      case MS_T_WK: dst = E.layers[layer].wqkv; rows = KD; cols = H; add = QD; break;
+      case MS_T_WV: dst = E.layers[layer].wqkv; rows = KD; cols = H; add = QD + KD; break;
+      case MS_T_WO: dst = E.layers[layer].wo; rows = H; cols = QD; break;
+      case MS_T_WGATE: dst = E.layers[layer].wgu; rows = E.F; cols = H; mul = 32; break;
+      case MS_T_WUP: dst = E.layers[layer].wgu; rows = E.F; cols = H; mul = 32; add = 16; break;
+      case MS_T_WDOWN: dst = E.layers[layer].wdown; rows = H; cols = E.F; break;
+      default: throw MsError(MS_EINVAL, "unknown tensor id " + std::to_string(tensor));
+    }
+    REQUIRE(n == (int64_t)rows * cols, MS_EINVAL,
+            "tensor " + std::to_string(tensor) + ": expected " + std::to_string((int64_t)rows * cols) +
+                " elements, got " + std::to_string(n));
+    if (rows == 1) {
+      HIP_OK(hipMemcpy(dst, host, (size_t)n * 2, hipMemcpyHostToDevice));
+      return MS_OK;
+    }
+    void* tmp = nullptr;
+    HIP_OK(hipMalloc(&tmp, (size_t)n * 2));
+    hipError_t ce = hipMemcpy(tmp, host, (size_t)n * 2, hipMemcpyHostToDevice);
+    if (ce == hipSuccess) {
+      launch_scatter_rows((const bf16_t*)tmp, dst, rows, cols, mul, add, E.stream);
+      ce = hipStreamSynchronize(E.stream);
+    }
+    (void)hipFree(tmp);
+    HIP_OK(ce);
+    return MS_OK;
+  });
+}
+
+int ms_init_synthetic(ms_engine* e, uint64_t seed, float std_, float jitter) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    HIP_OK(hipSetDevice(E.cfg.device));
+    const int H = E.H, QD = E.Hq * E.D, KD = E.Hk * E.D;
+    hipStream_t s = E.stream;
+    launch_synth_linear(E.embed, MS_T_EMBED, 0, E.V, H, seed, std_, 16, 0, s);
+    if (!E.cfg.tie_embeddings) launch_synth_linear(E.lm_head, MS_T_LM_HEAD, 0, E.V, H, seed, std_, 16, 0, s);
+    launch_synth_norm(E.final_norm, MS_T_FINAL_NORM, 0, H, seed, jitter, s);
+    for (int l = 0; l < E.L; ++l) {
+      Layer& Ly = E.layers[l];
+      launch_synth_norm(Ly.attn_norm, MS_T_ATTN_NORM, l, H, seed, jitter, s);
+      launch_synth_norm(Ly.ffn_norm, MS_T_FFN_NORM, l, H, seed, jitter, s);
+      launch_synth_linear(Ly.wqkv, MS_T_WQ, l, QD, H, seed, std_, 16, 0, s);
+      launch_synth_linear(Ly.wqkv, MS_T_WK, l, KD, H, seed, std_, 16, QD, s);
+      launch_synth_linear(Ly.wqkv, MS_T_WV, l, KD, H, seed, std_, 16, QD + KD, s);
+      launch_synth_linear(Ly.wo, MS_T_WO, l, H, QD, seed, std_, 16, 0, s);
+      launch_synth_linear(Ly.wgu, MS_T_WGATE, l, E.F, H, seed, std_, 32, 0, s);
+      launch_synth_linear(Ly.wgu, MS_T_WUP, l, E.F, H, seed, std_, 32, 16, s);
+      launch_synth_linear(Ly.wdown, MS_T_WDOWN, l, H, E.F, seed, std_, 16, 0, s);
+    }
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(s));
+    return MS_OK;
+  });
+}
+
+int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict, uint32_t flags,
+              uint64_t tag) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(ids != nullptr && n >= 1, MS_EINVAL, "empty prompt");
+    REQUIRE(num_predict >= 1, MS_EINVAL, "num_predict must be >= 1");
+    REQUIRE((int64_t)n + num_predict <= E.cfg.max_ctx, MS_ENOSPC,
+            "prompt (" + std::to_string(n) + ") + num_predict (" + std::to_string(num_predict) +
+                ") exceeds max_ctx " + std::to_string(E.cfg.max_ctx));
+    REQUIRE(n <= E.cfg.max_prefill_tokens, MS_ENOSPC, "prompt longer than max_prefill_tokens");
+    const int need = (n + num_predict + kPage - 1) / kPage;
+    REQUIRE(need <= E.n_pages, MS_ENOSPC, "request needs more KV pages than the pool holds");
+    for (int i = 0; i < n; ++i)
+      REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range at position " + std::to_string(i));
+    auto s = std::make_unique<Seq>();
+    s->tag = tag;
+    s->prompt.assign(ids, ids + n);
+    s->num_predict = num_predict;
+    s->flags = flags;
+    E.waiting.push_back(std::move(s));
+    return MS_OK;
+  });
+}
+
+int ms_pending(const ms_engine* e) {
+  if (!e) return MS_EINVAL;
+  return (int)(e->waiting.size() + e->running.size());
+}
+
+static bool is_eos(const ms_engine& E, int32_t t) {
+  for (int i = 0; i < E.cfg.n_eos; ++i)
+    if (E.cfg.eos_ids[i] == t) return true;
+  return false;
+}
+
+// returns true if the sequence finished with this token
+static bool accept_token(ms_engine& E, Seq& s, int32_t t) {
+  if (!(s.flags & MS_FLAG_IGNORE_EOS) && is_eos(E, t)) {
+    s.finish = MS_FINISH_EOS;
+    return true;
+  }
+  s.out.push_back(t);
+  if ((int)s.out.size() >= s.num_predict) {
+    s.finish = MS_FINISH_LENGTH;
+    return true;
+  }
+  return false;
+}
+
+static void release(ms_engine& E, Seq& s) {
+  for (int p : s.pages) E.free_pages.push_back(p);
+  s.pages.clear();
+  if (s.slot >= 0) E.free_slots.push_back(s.slot);
+  s.slot = -1;
+}
+
+static void reserve(ms_engine& E, Seq& s, int tokens) {
+  s.slot = E.free_slots.back();
+  E.free_slots.pop_back();
+  const int need = (tokens + kPage - 1) / kPage;
+  for (int i = 0; i < need; ++i) {
+    s.pages.push_back(E.free_pages.back());
+    E.free_pages.pop_back();
+  }
+  int32_t* row = &E.bt_h[(size_t)s.slot * E.max_pages];
+  for (int i = 0; i < need; ++i) row[i] = s.pages[i];
+  HIP_OK(hipMemcpyAsync(E.bt_d + (size_t)s.slot * E.max_pages, row, need * sizeof(int32_t),
+                        hipMemcpyHostToDevice, E.stream));
+}
+
+// packed varlen prefill of `batch` (fresh sequences); writes K/V, returns first greedy ids.
+// If n_layers_run < L: stops after that many layers (probe mode, no logits).
+static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, float* logits_all,
+                    std::vector<int32_t>* first_ids) {
+  const int S = (int)batch.size();
+  int T = 0;
+  for (Seq* s : batch) T += (int)s->prompt.size();
+  std::vector<int32_t> a;
+  a.reserve(4 * T + 8 * S + 64);
+  const size_t o_ids = a.size();
+  for (Seq* s : batch) a.insert(a.end(), s->prompt.begin(), s->prompt.end());
+  const size_t o_pos = a.size();
+  for (Seq* s : batch)
+    for (int i = 0; i < (int)s->prompt.size(); ++i) a.push_back(s->len + i);
+  const size_t o_slot = a.size();
+  for (Seq* s : batch)
+    for (int i = 0; i < (int)s->prompt.size(); ++i) a.push_back(s->slot);
+  const size_t o_qstart = a.size();
+  {
+    int q = 0;
+    for (Seq* s : batch) { a.push_back(q); q += (int)s->prompt.size(); }
+  }
+  const size_t o_qlen = a.size();
+  for (Seq* s : batch) a.push_back((int)s->prompt.size());
+  const size_t o_kvlen = a.size();
+  for (Seq* s : batch) a.push_back(s->len + (int)s->prompt.size());
+  const size_t o_sslot = a.size();
+  for (Seq* s : batch) a.push_back(s->slot);
+  const size_t o_last = a.size();
+  {
+    int q = 0;
+    for (Seq* s : batch) { q += (int)s->prompt.size(); a.push_back(q - 1); }
+  }
+  // q-blocks, heaviest (latest positions) first
+  std::vector<std::pair<int, int32_t>> qb;
+  for (int i = 0; i < S; ++i) {
+    const int n = (int)batch[i]->prompt.size();
+    for (int b = 0; b < (n + 63) / 64; ++b) qb.push_back({batch[i]->len + b * 64, (i << 16) | b});
+  }
+  std::stable_sort(qb.begin(), qb.end(), [](auto& x, auto& y) { return x.first > y.first; });
+  const size_t o_qblk = a.size();
+  for (auto& p : qb) a.push_back(p.second);
+  int32_t* d = E.upload_args(a);
+
+  PrefillAttnArgs pa;
+  pa.seq_qstart = d + o_qstart;
+  pa.seq_qlen = d + o_qlen;
+  pa.seq_kvlen = d + o_kvlen;
+  pa.seq_slot = d + o_sslot;
+  pa.qblk = d + o_qblk;
+  pa.n_qblk = (int)qb.size();
+  DecodeAttnArgs da{};
+
+  E.prof_begin(K_MISC);
+  launch_embed(d + o_ids, T, E.embed, E.H, E.x, E.stream);
+  E.prof_end(K_MISC);
+  for (int l = 0; l < n_layers_run; ++l) E.run_layer(l, T, false, d + o_pos, d + o_slot, pa, da);
+  HIP_OK(hipGetLastError());
+  if (n_layers_run < E.L) return;
+  if (!logits_all && !first_ids) return;  // probe of the final residual only
+  if (logits_all) {  // probe: logits of every position
+    launch_rmsnorm(E.x, E.final_norm, E.xb, T, E.H, E.cfg.norm_eps, nullptr, E.stream);
+    launch_gemm(E.xb, E.lm_head, logits_all, T, E.V, E.H, E.V, MS_EPI_STORE_F32, E.stream);
+    return;
+  }
+  E.prof_begin(K_MISC);
+  launch_rmsnorm(E.x, E.final_norm, E.xb, S, E.H, E.cfg.norm_eps, d + o_last, E.stream);
+  E.prof_end(K_MISC);
+  E.gemm_or_gemv(E.xb, E.lm_head, E.logits, S, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
+  E.prof_begin(K_MISC);
+  launch_argmax(E.logits, S, E.V, E.ids_out_d, E.stream);
+  E.prof_end(K_MISC);
+  HIP_OK(hipGetLastError());
+  first_ids->resize(S);
+  HIP_OK(hipMemcpyAsync(first_ids->data(), E.ids_out_d, S * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
+}
+
+// one greedy decode step for every running sequence (B rows of one token each)
+static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int32_t>& next) {
+  const int B = (int)batch.size();
+  std::vector<int32_t> a;
+  a.reserve(8 * B);
+  int max_len = 0;
+  const size_t o_ids = a.size();
+  for (Seq* s : batch) a.push_back(s->out.back());
+  const size_t o_pos = a.size();
+  for (Seq* s : batch) a.push_back(s->len);
+  const size_t o_slot = a.size();
+  for (Seq* s : batch) a.push_back(s->slot);
+  const size_t o_len = a.size();
+  for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
+  int32_t* d = E.upload_args(a);
+  DecodeAttnArgs da;
+  da.seq_len = d + o_len;
+  da.seq_slot = d + o_slot;
+  da.B = B;
+  da.max_len = max_len;
+  PrefillAttnArgs pa{};
+  E.prof_begin(K_MISC);
+  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
+  E.prof_end(K_MISC);
+  for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
+  E.prof_begin(K_MISC);
+  launch_rmsnorm(E.x, E.final_norm, E.xb, B, E.H, E.cfg.norm_eps, nullptr, E.stream);
+  E.prof_end(K_MISC);
+  E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
+  E.prof_begin(K_MISC);
+  launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
+  E.prof_end(K_MISC);
+  HIP_OK(hipGetLastError());
+  next.resize(B);
+  HIP_OK(hipMemcpyAsync(next.data(), E.ids_out_d, B * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
+}
+
+int ms_step(ms_engine* e) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    HIP_OK(hipSetDevice(E.cfg.device));
+    // 1. admit
+    std::vector<Seq*> admitted;
+    int budget = E.cfg.max_prefill_tokens;
+    while (!E.waiting.empty() && !E.free_slots.empty()) {
+      Seq& s = *E.waiting.front();
+      const int n = (int)s.prompt.size();
+      const int need = (n + s.num_predict + kPage - 1) / kPage;
+      if (need > (int)E.free_pages.size() || n > budget) break;
+      reserve(E, s, n + s.num_predict);
+      budget -= n;
+      admitted.push_back(&s);
+      E.running.push_back(std::move(E.waiting.front()));
+      E.waiting.pop_front();
+    }
+    // 2. prefill the admitted prompts
+    if (!admitted.empty()) {
+      std::vector<int32_t> first;
+      HIP_OK(hipEventRecord(E.ev_a, E.stream));
+      prefill(E, admitted, E.L, nullptr, &first);
+      HIP_OK(hipEventRecord(E.ev_b, E.stream));
+      HIP_OK(hipStreamSynchronize(E.stream));
+      float ms_ = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
+      E.stats.prefill_ms += ms_;
+      E.prof_collect();
+      E.stats.prefill_passes += 1;
+      for (size_t i = 0; i < admitted.size(); ++i) {
+        Seq& s = *admitted[i];
+        s.len = (int)s.prompt.size();
+        E.stats.prefill_tokens += s.len;
+        accept_token(E, s, first[i]);
+      }
+    }
+    // 3. one decode step for every running sequence that still needs tokens
+    std::vector<Seq*> batch;
+    for (auto& s : E.running)
+      if (!s->finish) batch.push_back(s.get());
+    for (size_t i0 = 0; i0 < batch.size(); i0 += 256) {
+      std::vector<Seq*> sub(batch.begin() + i0, batch.begin() + std::min(batch.size(), i0 + 256));
+      std::vector<int32_t> next;
+      HIP_OK(hipEventRecord(E.ev_a, E.stream));
+      decode_step(E, sub, next);
+      HIP_OK(hipEventRecord(E.ev_b, E.stream));
+      HIP_OK(hipStreamSynchronize(E.stream));
+      float ms_ = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
+      E.stats.decode_ms += ms_;
+      E.prof_collect();
+      E.stats.decode_steps += 1;
+      E.stats.decode_tokens += (int64_t)sub.size();
+      for (size_t i = 0; i < sub.size(); ++i) {
+        sub[i]->len += 1;
+        accept_token(E, *sub[i], next[i]);
+      }
+    }
+    // 4. retire finished sequences
+    for (auto it = E.running.begin(); it != E.running.end();) {
+      if ((*it)->finish) {
+        release(E, **it);
+        E.stats.finished += 1;
+        E.done.push_back(std::move(*it));
+        it = E.running.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    return (int)(E.waiting.size() + E.running.size());
+  });
+}
+
+int ms_poll(ms_engine* e, ms_result* out, int32_t cap) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(cap >= 0 && (cap == 0 || out != nullptr), MS_EINVAL, "bad poll buffer");
+    E.polled.clear();  // invalidates ids handed out by the previous poll
+    const int n = std::min<int>(cap, (int)E.done.size());
+    for (int i = 0; i < n; ++i) {
+      Seq& s = *E.done[i];
+      out[i].tag = s.tag;
+      out[i].ids = s.out.data();
+      out[i].n_ids = (int32_t)s.out.size();
+      out[i].finish_reason = s.finish;
+      out[i].n_prompt = (int32_t)s.prompt.size();
+      out[i]._pad = 0;
+    }
+    for (int i = 0; i < n; ++i) E.polled.push_back(std::move(E.done[i]));
+    E.done.erase(E.done.begin(), E.done.begin() + n);
+    return n;
+  });
+}
+
+int ms_get_stats(const ms_engine* e, ms_stats* out) {
+  if (!e || !out) return MS_EINVAL;
+  *out = e->stats;
+  return MS_OK;
+}
+
+int ms_reset_stats(ms_engine* e) {
+  if (!e) return MS_EINVAL;
+  e->stats = ms_stats{};
+  return MS_OK;
+}
+
+int ms_set_profiling(ms_engine* e, uint32_t mask) {
+  if (!e) return MS_EINVAL;
+  e->prof_mask = mask;
+  return MS_OK;
+}
+
+int ms_synchronize(ms_engine* e) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    HIP_OK(hipStreamSynchronize(e->stream));
+    return MS_OK;
+  });
+}
+
+int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run, float* hidden_out,
+               float* logits_out) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    HIP_OK(hipSetDevice(E.cfg.device));
+    REQUIRE(E.waiting.empty() && E.running.empty(), MS_EBUSY, "ms_forward needs an idle engine");
+    REQUIRE(ids && n >= 1 && n <= E.cfg.max_prefill_tokens && n <= E.cfg.max_ctx, MS_EINVAL, "bad probe length");
+    REQUIRE(n_layers_run >= 0 && n_layers_run <= E.L, MS_EINVAL, "n_layers_run out of range");
+    REQUIRE(!logits_out || n_layers_run == E.L, MS_EINVAL, "logits need every layer");
+    REQUIRE((n + kPage - 1) / kPage <= (int)E.free_pages.size(), MS_ENOSPC, "not enough KV pages");
+    for (int i = 0; i < n; ++i) REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range");
+    Seq s;
+    s.prompt.assign(ids, ids + n);
+    reserve(E, s, n);
+    std::vector<Seq*> b{&s};
+    float* lg = nullptr;
+    int rc = MS_OK;
+    try {
+      if (logits_out) {
+        HIP_OK(hipMalloc((void**)&lg, (size_t)n * E.V * sizeof(float)));
+      }
+      prefill(E, b, n_layers_run, lg, nullptr);
+      HIP_OK(hipStreamSynchronize(E.stream));
+      if (hidden_out)
+        HIP_OK(hipMemcpy(hidden_out, E.x, (size_t)n * E.H * sizeof(float), hipMemcpyDeviceToHost));
+      if (logits_out)
+        HIP_OK(hipMemcpy(logits_out, lg, (size_t)n * E.V * sizeof(float), hipMemcpyDeviceToHost));
+    } catch (...) {
+      if (lg) (void)hipFree(lg);
+      release(E, s);
+      throw;
+    }
+    if (lg) (void)hipFree(lg);
+    release(E, s);
+    E.ev_pending.clear();
+    E.ev_used = 0;
+    return rc;
+  });
+}
+
+// ---------------------------------------------------------------------------- op entry points
+static int op_guard(const std::function<void()>& fn) {
+  try {
+    fn();
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) {
+      g_last_error = std::string("kernel launch failed: ") + hipGetErrorString(err);
+      return MS_EIO;
+    }
+    return MS_OK;
+  } catch (const MsError& x) {
+    g_last_error = x.what();
+    return x.code;
+  }
+}
+
+int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t ldo,
+               int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
+    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    launch_gemm((const bf16_t*)A, (const bf16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream);
+  });
+}
+
+int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K) {
+  if (M < 1 || M > 64 || N < 16 || K < 256 || K % 256) return MS_EINVAL;
+  return (int64_t)gemv_workspace_bytes(M, N, K);
+}
+
+int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t ldo,
+               int32_t epi, void* ws, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && W && out && ws && M >= 1 && M <= 64 && N >= 16 && N % 16 == 0 && K >= 256 &&
+                K % 256 == 0,
+            MS_EINVAL, "bad gemv shape (M<=64, N%16==0, K%256==0)");
+    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    launch_gemv((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, ws, (hipStream_t)stream);
+  });
+}
+
+int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
+                  const int32_t* row_idx, void* stream) {
+  return op_guard([&] {
+    REQUIRE(x && w && y && rows >= 1 && hidden >= 4 && hidden % 4 == 0, MS_EINVAL, "bad rmsnorm shape");
+    launch_rmsnorm((const float*)x, (const bf16_t*)w, (bf16_t*)y, rows, hidden, eps, row_idx,
+                   (hipStream_t)stream);
+  });
+}
+
+int ms_op_argmax(const void* logits, int32_t rows, int32_t n, int32_t* ids, void* stream) {
+  return op_guard([&] {
+    REQUIRE(logits && ids && rows >= 1 && n >= 1, MS_EINVAL, "bad argmax shape");
+    launch_argmax((const float*)logits, rows, n, ids, (hipStream_t)stream);
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,352 @@
+// k_attn.hip -- causal GQA attention of the map call over the paged KV cache.
+//
+// Replaces ggml's attention (mul_mat+soft_max / flash_attn_ext) inside Ollama
+// (SURVEY.md §2 'ggml op replaced', §8a rows A8/A9).  head_dim 128, any GQA group.
+//
+// KV cache: pool[page][kv_head][64 tokens][128] bf16, one page = one 64-key tile;
+// a per-sequence block table maps logical tile -> page (engine.cpp owns the pages).
+//
+// Both kernels use the "swapped" orientation on v_mfma_f32_16x16x32_bf16:
+//   S^T = K . Q^T     (A = K rows from LDS/HBM, B = Q fragments held in VGPRs)
+//   O^T += V^T . P^T  (A = V^T via ds_read_b64_tr_b16 from a row-major V tile,
+//                      B = P^T taken straight from the S^T accumulators)
+// so the query index sits on the MFMA column (lane & 15) in S^T, P^T and O^T alike:
+// the online-softmax max/sum need only two lane-xor shuffles and the O rescale is
+// lane-local.  The k order inside a PV step is permuted (keys 4g..4g+3 and
+// 16+4g..16+4g+3 for lane group g), identically on both operands.
+// LDS images: K rows swizzled chunk ^ (row & 15) (ds_read_b128, conflict-free);
+// V rows swizzled chunk ^ ((row & 7) << 1) (tr reads conflict-free).
+#include "kernels.h"
+
+namespace ms {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+__device__ __forceinline__ int k_swz(int row, int ch) { return row * 256 + ((ch ^ (row & 15)) << 4); }
+__device__ __forceinline__ int v_swz(int row, int ch) { return row * 256 + ((ch ^ ((row & 7) << 1)) << 4); }
+
+// A operand of O^T += V^T P^T for d-tile dt, k-step ks: two transposed 4x16 reads.
+__device__ __forceinline__ bf16x8 load_vt(const char* vs, int dt, int ks, int lane) {
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
+  const int r0 = 32 * ks + 4 * g + q, r1 = r0 + 16;
+  const int ch = 2 * dt + (p >> 1), sub = (p & 1) * 8;
+  typedef short s4 __attribute__((ext_vector_type(4)));
+  s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4*)(vs + v_swz(r0, ch) + sub));
+  s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4*)(vs + v_swz(r1, ch) + sub));
+  typedef short s8 __attribute__((ext_vector_type(8)));
+  s8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+// B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1
+__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  u4 v = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+// one 64-key K/V tile (16 KB each) into registers, 4 x 16 B per thread, coalesced rows
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], const KVView& kv,
+                                              const int32_t* bt, int kvh, int t, int kvlen,
+                                              int tid) {
+  const size_t base = ((size_t)bt[t] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  const int row = tid >> 4, ch = tid & 15;
+  kr[0] = *(const u32x4*)(kv.k + base + (row + 0) * kHeadDim + ch * 8);
+  kr[1] = *(const u32x4*)(kv.k + base + (row + 16) * kHeadDim + ch * 8);
+  kr[2] = *(const u32x4*)(kv.k + base + (row + 32) * kHeadDim + ch * 8);
+  kr[3] = *(const u32x4*)(kv.k + base + (row + 48) * kHeadDim + ch * 8);
+  vr[0] = *(const u32x4*)(kv.v + base + (row + 0) * kHeadDim + ch * 8);
+  vr[1] = *(const u32x4*)(kv.v + base + (row + 16) * kHeadDim + ch * 8);
+  vr[2] = *(const u32x4*)(kv.v + base + (row + 32) * kHeadDim + ch * 8);
+  vr[3] = *(const u32x4*)(kv.v + base + (row + 48) * kHeadDim + ch * 8);
+  const int lim = kvlen - t * 64;  // rows >= lim are past the sequence: never feed stale V to P.V
+  if (row + 0 >= lim) vr[0] = u32x4{0, 0, 0, 0};
+  if (row + 16 >= lim) vr[1] = u32x4{0, 0, 0, 0};
+  if (row + 32 >= lim) vr[2] = u32x4{0, 0, 0, 0};
+  if (row + 48 >= lim) vr[3] = u32x4{0, 0, 0, 0};
+}
+
+// ============================================================ prefill (varlen, causal)
+// grid (n_qblk, Hq); block 256 = 4 waves x 16 query rows of one head; KV tiles of 64.
+__global__ __launch_bounds__(256) void attn_prefill_kernel(const bf16_t* __restrict__ qkv,
+                                                           bf16_t* __restrict__ out, int Hq,
+                                                           int Hk, KVView kv, PrefillAttnArgs a,
+                                                           float scale_log2) {
+  __shared__ __attribute__((aligned(16))) char smem[32768];
+  char* ks_ = smem;
+  char* vs_ = smem + 16384;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int h = blockIdx.y;
+  const int e = a.qblk[blockIdx.x];
+  const int sq = e >> 16, qb = e & 0xFFFF;
+  const int qlen = a.seq_qlen[sq], kvlen = a.seq_kvlen[sq], qstart = a.seq_qstart[sq];
+  const int slot = a.seq_slot[sq];
+  const int kvh = h / (Hq / Hk);
+  const int row_stride = (Hq + 2 * Hk) * kHeadDim;
+  const int qi = qb * 64 + wave * 16 + r;
+  const int qpos = kvlen - qlen + qi;
+
+  bf16x8 qf[4];
+  {
+    const bf16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h * kHeadDim;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int q_last = min(qb * 64 + 63, qlen - 1);
+  const int kv_end = kvlen - qlen + q_last + 1;  // keys visible to the block's last query
+  const int ntiles = (kv_end + 63) / 64;
+  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
+
+  u32x4 kreg[4], vreg[4];
+  fetch_kv_tile(kreg, vreg, kv, bt, kvh, 0, kvlen, tid);
+  for (int t = 0; t < ntiles; ++t) {
+    __syncthreads();  // previous tile fully consumed
+    {
+      const int row = tid >> 4, ch = tid & 15;
+      *(u32x4*)(ks_ + k_swz(row, ch)) = kreg[0];
+      *(u32x4*)(ks_ + k_swz(row + 16, ch)) = kreg[1];
+      *(u32x4*)(ks_ + k_swz(row + 32, ch)) = kreg[2];
+      *(u32x4*)(ks_ + k_swz(row + 48, ch)) = kreg[3];
+      *(u32x4*)(vs_ + v_swz(row, ch)) = vreg[0];
+      *(u32x4*)(vs_ + v_swz(row + 16, ch)) = vreg[1];
+      *(u32x4*)(vs_ + v_swz(row + 32, ch)) = vreg[2];
+      *(u32x4*)(vs_ + v_swz(row + 48, ch)) = vreg[3];
+    }
+    __syncthreads();
+    if (t + 1 < ntiles) fetch_kv_tile(kreg, vreg, kv, bt, kvh, t + 1, kvlen, tid);  // next tile's HBM reads overlap this tile's math
+
+    f32x4 sc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int krow = mt * 16 + r;
+        const bf16x8 kf = *(const bf16x8*)(ks_ + k_swz(krow, 4 * s + g));
+        sc[mt] = mfma16(kf, qf[s], sc[mt]);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = t * 64 + mt * 16 + 4 * g + j;
+        const float v = (key > qpos || key >= kvlen) ? -INFINITY : sc[mt][j] * scale_log2;
+        sc[mt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - m_new);
+        sc[mt][j] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+#pragma unroll
+    for (int kstep = 0; kstep < 2; ++kstep) {
+      const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
+    }
+  }
+  if (qi < qlen) {
+    const float inv = 1.0f / l_run;
+    bf16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + h * kHeadDim;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 w;
+      w.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
+      w.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
+      *(uint2*)(orow + dt * 16 + 4 * g) = w;
+    }
+  }
+}
+
+void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+                         PrefillAttnArgs a, hipStream_t s) {
+  if (a.n_qblk <= 0) return;
+  const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
+  hipLaunchKernelGGL(attn_prefill_kernel, dim3(a.n_qblk, Hq), dim3(256), 0, s, qkv, out, Hq, Hk,
+                     kv, a, scale_log2);
+}
+
+// ============================================================ decode (split-K over keys)
+// grid (B, Hk, nsplit); block 256 = 4 waves; each wave owns pages of the split in
+// round robin and keeps its own online softmax for the G query heads of its kv head
+// (MFMA columns 0..G-1).  Partial (m, l, o[128]) per (b, q head, split) -> combine.
+constexpr int kSplitPages = 4;  // 256 keys per block
+
+size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
+  const int nsplit = (max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
+  return (size_t)B * Hq * nsplit * 132 * sizeof(float);
+}
+
+__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ qkv, int Hq,
+                                                          int Hk, KVView kv, DecodeAttnArgs a,
+                                                          float* __restrict__ ws, int nsplit,
+                                                          float scale_log2) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 4 * 16 * 130 * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int b = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
+  const int G = Hq / Hk;
+  const int len = a.seq_len[b];
+  const int slot = a.seq_slot[b];
+  const int row_stride = (Hq + 2 * Hk) * kHeadDim;
+  char* vs_ = smem + wave * 16384;
+  float* mrg = (float*)(smem + 4 * 16384);  // [wave][16 cols][130] m, l, o[128]
+
+  bf16x8 qf[4];
+  {
+    const int hq = kvh * G + min(r, G - 1);
+    const bf16_t* qrow = qkv + (size_t)b * row_stride + hq * kHeadDim;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
+  }
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
+  const int page_lo = split * kSplitPages;
+  const int npages = (len + kPage - 1) / kPage;
+  for (int pg = page_lo + wave; pg < min(page_lo + kSplitPages, npages); pg += 4) {
+    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+    // V page -> this wave's LDS (rows past len zeroed)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int c = i * 64 + lane, row = c >> 4, ch = c & 15;
+      u32x4 v = *(const u32x4*)(kv.v + base + row * kHeadDim + ch * 8);
+      if (pg * kPage + row >= len) v = u32x4{0, 0, 0, 0};
+      *(u32x4*)(vs_ + v_swz(row, ch)) = v;
+    }
+    // S^T = K . Q^T with K straight from HBM (16 rows x 64 B per wave-instruction)
+    f32x4 sc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bf16_t* krow = kv.k + base + (mt * 16 + r) * kHeadDim + 8 * g;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) sc[mt] = mfma16(as_bf16x8(*(const uint4*)(krow + 32 * s)), qf[s], sc[mt]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = pg * kPage + mt * 16 + 4 * g + j;
+        const float v = (key >= len) ? -INFINITY : sc[mt][j] * scale_log2;
+        sc[mt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - m_new);
+        sc[mt][j] = p;
+        rs += p;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V tile is in LDS
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kstep = 0; kstep < 2; ++kstep) {
+      const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  // merge the 4 waves: each wave publishes (m, l, O^T) for its 16 columns
+  {
+    float* mw = mrg + wave * 16 * 130;
+    if (g == 0) { mw[r * 130 + 0] = m_run; mw[r * 130 + 1] = l_run; }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mw[r * 130 + 2 + dt * 16 + 4 * g + j] = o[dt][j];
+  }
+  __syncthreads();
+  // threads: col c < G, d in [0,128): 2 d per thread over 256 threads -> G*128 outputs
+  for (int idx = tid; idx < G * 130; idx += 256) {
+    const int c = idx / 130, k = idx % 130;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, mrg[(w * 16 + c) * 130]);
+    float acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float mw = mrg[(w * 16 + c) * 130];
+      const float f = (mw == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(mw - M);
+      const float v = mrg[(w * 16 + c) * 130 + k];
+      acc += (k == 0) ? 0.f : f * v;
+    }
+    const int hq = kvh * G + c;
+    float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;
+    dst[k] = (k == 0) ? M : acc;
+  }
+}
+
+// out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s,  w_s = 2^(m_s - max m)
+__global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
+                                                                  bf16_t* __restrict__ out, int Hq,
+                                                                  int nsplit) {
+  const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  const float* p = ws + ((size_t)b * Hq + hq) * nsplit * 132;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, p[s * 132]);
+  float L = 0.f, O = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float ms_ = p[s * 132];
+    if (ms_ == -INFINITY) continue;
+    const float f = __builtin_amdgcn_exp2f(ms_ - M);
+    L += f * p[s * 132 + 1];
+    O += f * p[s * 132 + 2 + d];
+  }
+  out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2bf(O / L);
+}
+
+void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+                        DecodeAttnArgs a, float* ws, hipStream_t s) {
+  if (a.B <= 0) return;
+  const int nsplit = (a.max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
+  const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
+  hipLaunchKernelGGL(attn_decode_kernel, dim3(a.B, Hk, nsplit), dim3(256), 0, s, qkv, Hq, Hk, kv,
+                     a, ws, nsplit, scale_log2);
+  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq,
+                     nsplit);
+}
+
+}  // namespace ms

@@ -1,0 +1,257 @@
+// k_misc.hip -- HBM-bound helper kernels of the map call: embedding gather, RMSNorm,
+// RoPE + paged-KV scatter, greedy argmax, synthetic weights.
+//
+// Reference semantics (EXT, inside Ollama for one /api/generate, SURVEY.md §2 table
+// "ggml op replaced"): get_rows, rms_norm+mul, rope (llama3 freq factors), the greedy
+// sampler.  Numerics contract restated in oracle/llama_ref.py.
+#include "kernels.h"
+
+namespace ms {
+
+// ---------------------------------------------------------------- embedding
+// x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores
+__global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
+                                                    const bf16_t* __restrict__ emb, int H,
+                                                    float* __restrict__ x) {
+  const int t = blockIdx.x;
+  const bf16_t* row = emb + (size_t)ids[t] * H;
+  float* xo = x + (size_t)t * H;
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
+    uint4 v = *(const uint4*)(row + c * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    float4 a, b;
+    a.x = __uint_as_float(w[0] << 16); a.y = __uint_as_float(w[0] & 0xFFFF0000u);
+    a.z = __uint_as_float(w[1] << 16); a.w = __uint_as_float(w[1] & 0xFFFF0000u);
+    b.x = __uint_as_float(w[2] << 16); b.y = __uint_as_float(w[2] & 0xFFFF0000u);
+    b.z = __uint_as_float(w[3] << 16); b.w = __uint_as_float(w[3] & 0xFFFF0000u);
+    *(float4*)(xo + c * 8) = a;
+    *(float4*)(xo + c * 8 + 4) = b;
+  }
+}
+
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
+  if (T <= 0) return;
+  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
+}
+
+// ---------------------------------------------------------------- RMSNorm
+// y = bf16( (x * rsqrt(mean(x^2) + eps)) * w ), one 256-thread block per row.
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x,
+                                                      const bf16_t* __restrict__ w,
+                                                      bf16_t* __restrict__ y, int H, float eps,
+                                                      const int32_t* __restrict__ row_idx) {
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  const int src = row_idx ? row_idx[r] : r;
+  const float* xr = x + (size_t)src * H;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < H / 4; c += 256) {
+    float4 v = *(const float4*)(xr + c * 4);
+    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float rinv = 1.0f / sqrtf(tot / (float)H + eps);
+  bf16_t* yr = y + (size_t)r * H;
+  for (int c = threadIdx.x; c < H / 4; c += 256) {
+    float4 v = *(const float4*)(xr + c * 4);
+    uint2 wv = *(const uint2*)(w + c * 4);
+    float g0 = __uint_as_float(wv.x << 16), g1 = __uint_as_float(wv.x & 0xFFFF0000u);
+    float g2 = __uint_as_float(wv.y << 16), g3 = __uint_as_float(wv.y & 0xFFFF0000u);
+    uint2 o;
+    o.x = pack2bf((v.x * rinv) * g0, (v.y * rinv) * g1);
+    o.y = pack2bf((v.z * rinv) * g2, (v.w * rinv) * g3);
+    *(uint2*)(yr + c * 4) = o;
+  }
+}
+
+void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
+                    const int32_t* row_idx, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, H, eps, row_idx);
+}
+
+// ---------------------------------------------------------------- RoPE + KV scatter
+// qkv row layout: [Q heads | K heads | V heads] x 128.  rotate-half pairs (i, i+64).
+// One block per token; a thread owns 4 consecutive pair indices of one head.
+__global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, int Hq, int Hk,
+                                                      const int32_t* __restrict__ tok_pos,
+                                                      const int32_t* __restrict__ tok_slot,
+                                                      const float* __restrict__ cos_tab,
+                                                      const float* __restrict__ sin_tab,
+                                                      KVView kv) {
+  const int t = blockIdx.x;
+  const int pos = tok_pos[t];
+  const int slot = tok_slot[t];
+  const int page = kv.block_table[(size_t)slot * kv.max_pages + pos / kPage];
+  const int off = pos % kPage;
+  const int row_elems = (Hq + 2 * Hk) * kHeadDim;
+  bf16_t* row = qkv + (size_t)t * row_elems;
+  const int items = (Hq + 2 * Hk) * 16;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int head = it >> 4;
+    const int i0 = (it & 15) * 4;
+    bf16_t* hp = row + head * kHeadDim;
+    uint2 lo = *(const uint2*)(hp + i0);
+    uint2 hi = *(const uint2*)(hp + i0 + 64);
+    uint2 olo = lo, ohi = hi;
+    if (head < Hq + Hk) {  // Q or K: rotate
+      const float4 c = *(const float4*)(cos_tab + (size_t)pos * 64 + i0);
+      const float4 sn = *(const float4*)(sin_tab + (size_t)pos * 64 + i0);
+      float a[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xFFFF0000u),
+                    __uint_as_float(lo.y << 16), __uint_as_float(lo.y & 0xFFFF0000u)};
+      float b[4] = {__uint_as_float(hi.x << 16), __uint_as_float(hi.x & 0xFFFF0000u),
+                    __uint_as_float(hi.y << 16), __uint_as_float(hi.y & 0xFFFF0000u)};
+      const float cc[4] = {c.x, c.y, c.z, c.w};
+      const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
+      float ra[4], rb[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        ra[j] = __fsub_rn(__fmul_rn(a[j], cc[j]), __fmul_rn(b[j], ss[j]));
+        rb[j] = __fadd_rn(__fmul_rn(b[j], cc[j]), __fmul_rn(a[j], ss[j]));
+      }
+      olo.x = pack2bf(ra[0], ra[1]); olo.y = pack2bf(ra[2], ra[3]);
+      ohi.x = pack2bf(rb[0], rb[1]); ohi.y = pack2bf(rb[2], rb[3]);
+    }
+    if (head < Hq) {
+      *(uint2*)(hp + i0) = olo;
+      *(uint2*)(hp + i0 + 64) = ohi;
+    } else {
+      const bool is_k = head < Hq + Hk;
+      const int kh = is_k ? head - Hq : head - Hq - Hk;
+      bf16_t* dst = (is_k ? kv.k : kv.v) +
+                    (((size_t)page * kv.n_kv_heads + kh) * kPage + off) * kHeadDim;
+      *(uint2*)(dst + i0) = olo;
+      *(uint2*)(dst + i0 + 64) = ohi;
+    }
+  }
+}
+
+void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
+                    const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
+                    KVView kv, hipStream_t s) {
+  if (T <= 0) return;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, s, qkv, Hq, Hk, tok_pos, tok_slot,
+                     cos_tab, sin_tab, kv);
+}
+
+// ---------------------------------------------------------------- greedy argmax
+// Ollama T=0 / top_k=1 semantics; ties resolve to the lowest id (oracle: np.argmax).
+__device__ __forceinline__ void amax_merge(float& v, int& i, float v2, int i2) {
+  if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+
+__global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ logits, int n,
+                                                      int32_t* __restrict__ out) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const float* row = logits + (size_t)blockIdx.x * n;
+  float v = -INFINITY;
+  int idx = 0x7FFFFFFF;
+  const int n4 = n / 4;
+  for (int c = threadIdx.x; c < n4; c += 1024) {
+    float4 q = *(const float4*)(row + c * 4);
+    amax_merge(v, idx, q.x, c * 4);
+    amax_merge(v, idx, q.y, c * 4 + 1);
+    amax_merge(v, idx, q.z, c * 4 + 2);
+    amax_merge(v, idx, q.w, c * 4 + 3);
+  }
+  for (int c = n4 * 4 + threadIdx.x; c < n; c += 1024) amax_merge(v, idx, row[c], c);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    float v2 = __shfl_xor(v, o, 64);
+    int i2 = __shfl_xor(idx, o, 64);
+    amax_merge(v, idx, v2, i2);
+  }
+  if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; si[threadIdx.x >> 6] = idx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) amax_merge(v, idx, sv[w], si[w]);
+    out[blockIdx.x] = idx == 0x7FFFFFFF ? 0 : idx;
+  }
+}
+
+void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s) {
+  if (rows <= 0) return;
+  hipLaunchKernelGGL(argmax_kernel, dim3(rows), dim3(1024), 0, s, logits, n, out);
+}
+
+// ---------------------------------------------------------------- synthetic weights
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ int limb_sum(uint64_t seed_h, int kind, int layer, int r, int c) {
+  const uint64_t key = ((uint64_t)kind << 58) | ((uint64_t)layer << 50) | ((uint64_t)r << 20) |
+                       (uint64_t)c;
+  const uint64_t h = splitmix64(key ^ seed_h);
+  return (int)((h & 0xFFFF) + ((h >> 16) & 0xFFFF) + ((h >> 32) & 0xFFFF) + ((h >> 48) & 0xFFFF)) -
+         131070;
+}
+
+__device__ __forceinline__ bf16_t rne_bits(float f) {  // integer RNE, finite inputs only
+  const uint32_t u = __float_as_uint(f);
+  return (bf16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+__global__ void synth_linear_kernel(bf16_t* dst, int kind, int layer, int rows, int cols,
+                                    uint64_t seed_h, float scale, int map_mul, int map_add) {
+  const size_t n = (size_t)rows * cols;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(e / cols), c = (int)(e % cols);
+    const float v = __fmul_rn((float)limb_sum(seed_h, kind, layer, r, c), scale);
+    const size_t dr = (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
+    dst[dr * cols + c] = rne_bits(v);
+  }
+}
+
+__global__ void synth_norm_kernel(bf16_t* dst, int kind, int layer, int n, uint64_t seed_h,
+                                  float scale) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
+    const float v = __fadd_rn(1.0f, __fmul_rn((float)limb_sum(seed_h, kind, layer, 0, c), scale));
+    dst[c] = rne_bits(v);
+  }
+}
+
+static uint64_t host_splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
+                         float std, int map_mul, int map_add, hipStream_t s) {
+  // scale = float32(std*sqrt(3)/65536), computed in double then rounded once (as numpy does)
+  const float scale = (float)((double)std * 1.7320508075688772 / 65536.0);
+  hipLaunchKernelGGL(synth_linear_kernel, dim3(2048), dim3(256), 0, s, dst, kind, layer, rows,
+                     cols, host_splitmix64(seed), scale, map_mul, map_add);
+}
+
+void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
+                       hipStream_t s) {
+  const float scale = (float)((double)jitter / 131070.0);
+  hipLaunchKernelGGL(synth_norm_kernel, dim3(16), dim3(256), 0, s, dst, kind, layer, n,
+                     host_splitmix64(seed), scale);
+}
+
+__global__ void scatter_rows_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+                                    int rows, int cols, int map_mul, int map_add) {
+  const int r = blockIdx.x;
+  const size_t dr = (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) dst[dr * cols + c] = src[(size_t)r * cols + c];
+}
+
+void launch_scatter_rows(const bf16_t* src, bf16_t* dst, int rows, int cols, int map_mul,
+                         int map_add, hipStream_t s) {
+  hipLaunchKernelGGL(scatter_rows_kernel, dim3(rows), dim3(256), 0, s, src, dst, rows, cols,
+                     map_mul, map_add);
+}
+
+}  // namespace ms

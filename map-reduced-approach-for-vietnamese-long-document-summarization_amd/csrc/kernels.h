@@ -1,0 +1,65 @@
+// kernels.h -- launchers for the gfx950 map-phase kernels (host-callable).
+#pragma once
+#include "common.h"
+
+namespace ms {
+
+// Where the K/V of one layer live: pool[page][kv_head][64 tokens][128] bf16.
+struct KVView {
+  bf16_t* k;
+  bf16_t* v;
+  const int32_t* block_table;  // [slots][max_pages]
+  int32_t max_pages;           // row stride of block_table
+  int32_t n_kv_heads;
+};
+
+// Prefill attention work description (device arrays, see engine.cpp StepArgs).
+struct PrefillAttnArgs {
+  const int32_t* seq_qstart;  // [S] row of the sequence's first query token in qkv
+  const int32_t* seq_qlen;    // [S]
+  const int32_t* seq_kvlen;   // [S] keys visible to the last query (= cached + qlen)
+  const int32_t* seq_slot;    // [S] block-table row
+  const int32_t* qblk;        // [NQB] (seq << 16) | q_block, heaviest first
+  int32_t n_qblk;
+};
+
+struct DecodeAttnArgs {
+  const int32_t* seq_len;   // [B] keys incl. the new token
+  const int32_t* seq_slot;  // [B]
+  int32_t B;
+  int32_t max_len;          // upper bound over the batch (sets the split grid)
+};
+
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
+void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
+                    const int32_t* row_idx, hipStream_t s);
+// RoPE on Q (in place) and K; K,V scattered into the paged cache.
+void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
+                    const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
+                    KVView kv, hipStream_t s);
+void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s);
+
+// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0
+void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                 int epi, hipStream_t s);
+// M <= 64 decode variant; ws: fp32 split-K slabs + tickets (see gemv_workspace_bytes)
+size_t gemv_workspace_bytes(int M, int N, int K);
+void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                 int epi, void* ws, hipStream_t s);
+
+void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+                         PrefillAttnArgs a, hipStream_t s);
+size_t attn_decode_workspace_bytes(int B, int Hq, int max_len);
+void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+                        DecodeAttnArgs a, float* ws, hipStream_t s);
+
+// synthetic weights (oracle/synth.py restates this generator)
+void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
+                         float std, int map_mul, int map_add, hipStream_t s);
+void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
+                       hipStream_t s);
+// scatter a logical [rows][cols] tensor into a fused/interleaved physical layout
+void launch_scatter_rows(const bf16_t* src, bf16_t* dst, int rows, int cols, int map_mul,
+                         int map_add, hipStream_t s);
+
+}  // namespace ms

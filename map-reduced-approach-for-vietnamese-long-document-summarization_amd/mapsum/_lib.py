@@ -1,0 +1,107 @@
+"""ctypes binding of libmapsum.so (C-ABI declared in include/mapsum.h).
+
+The library is built in-tree (``make -C csrc`` / ``__graft_entry__.build()``).  There
+is no fallback: if it is missing or fails to load, ``load()`` raises, so the product
+path can never silently run on anything but the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmapsum.so")
+
+MS_ABI_VERSION = 1
+MS_OK, MS_EIO, MS_ENOMEM, MS_EBUSY, MS_EINVAL, MS_ENOSPC = 0, -5, -12, -16, -22, -28
+MS_FINISH_EOS, MS_FINISH_LENGTH, MS_FINISH_ERROR = 1, 2, 3
+MS_FLAG_IGNORE_EOS = 1
+(MS_T_EMBED, MS_T_ATTN_NORM, MS_T_WQ, MS_T_WK, MS_T_WV, MS_T_WO, MS_T_FFN_NORM, MS_T_WGATE,
+ MS_T_WUP, MS_T_WDOWN, MS_T_FINAL_NORM, MS_T_LM_HEAD) = range(12)
+MS_EPI_STORE_BF16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
+# kernel classes of ms_stats.kernel_ms
+K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC = range(6)
+
+EXPORTED = (
+    "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
+    "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
+    "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
+    "ms_op_gemv", "ms_op_rmsnorm", "ms_op_argmax",
+)
+
+
+class MsConfig(C.Structure):
+    _fields_ = [("abi_version", C.c_int32),
+                ("n_layers", C.c_int32), ("hidden", C.c_int32), ("n_heads", C.c_int32),
+                ("n_kv_heads", C.c_int32), ("head_dim", C.c_int32), ("ffn", C.c_int32),
+                ("vocab", C.c_int32),
+                ("rope_theta", C.c_float), ("rope_factor", C.c_float),
+                ("rope_low_freq_factor", C.c_float), ("rope_high_freq_factor", C.c_float),
+                ("rope_orig_ctx", C.c_int32), ("norm_eps", C.c_float), ("tie_embeddings", C.c_int32),
+                ("device", C.c_int32), ("max_batch", C.c_int32), ("max_ctx", C.c_int32),
+                ("max_prefill_tokens", C.c_int32), ("n_pages", C.c_int32), ("n_eos", C.c_int32),
+                ("eos_ids", C.c_int32 * 8)]
+
+
+class MsResult(C.Structure):
+    _fields_ = [("tag", C.c_uint64), ("ids", C.POINTER(C.c_int32)), ("n_ids", C.c_int32),
+                ("finish_reason", C.c_int32), ("n_prompt", C.c_int32), ("_pad", C.c_int32)]
+
+
+class MsStats(C.Structure):
+    _fields_ = [("prefill_tokens", C.c_int64), ("decode_tokens", C.c_int64),
+                ("prefill_passes", C.c_int64), ("decode_steps", C.c_int64), ("finished", C.c_int64),
+                ("prefill_ms", C.c_double), ("decode_ms", C.c_double),
+                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libmapsum.so (raises if it was not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libmapsum.so not found at {LIB_PATH}; build it with "
+                           f"`make -C csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(LIB_PATH)
+    vp, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+    pi32 = C.POINTER(C.c_int32)
+    sig = {
+        "ms_create": (i32, [C.POINTER(MsConfig), C.POINTER(vp)]),
+        "ms_destroy": (i32, [vp]),
+        "ms_last_error": (C.c_char_p, [vp]),
+        "ms_load_weight": (i32, [vp, i32, i32, vp, i64]),
+        "ms_init_synthetic": (i32, [vp, u64, C.c_float, C.c_float]),
+        "ms_submit": (i32, [vp, pi32, i32, i32, u32, u64]),
+        "ms_step": (i32, [vp]),
+        "ms_poll": (i32, [vp, C.POINTER(MsResult), i32]),
+        "ms_pending": (i32, [vp]),
+        "ms_get_stats": (i32, [vp, C.POINTER(MsStats)]),
+        "ms_reset_stats": (i32, [vp]),
+        "ms_set_profiling": (i32, [vp, u32]),
+        "ms_synchronize": (i32, [vp]),
+        "ms_forward": (i32, [vp, pi32, i32, i32, vp, vp]),
+        "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+        "ms_op_gemv_workspace": (i64, [i32, i32, i32]),
+        "ms_op_gemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
+        "ms_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, C.c_float, vp, vp]),
+        "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, handle=None, what: str = "") -> int:
+    """Raise RuntimeError on a negative status (mirrors resp.raise_for_status(),
+    run_full_evaluation_pipeline.py:91)."""
+    if rc < 0:
+        msg = load().ms_last_error(handle)
+        raise RuntimeError(f"libmapsum {what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc

@@ -1,0 +1,158 @@
+"""Python handle on one libmapsum engine (one GPU, one process).
+
+The reference makes one blocking HTTP generate per chunk
+(run_full_evaluation_pipeline.py:80-106).  Here the same unit of work -- prompt ids
+in, greedy summary ids out, stop at an end-of-turn id or ``num_predict`` -- is a
+``submit``; ``step`` advances every submitted chunk together (continuous batching
+inside libmapsum), ``poll`` returns finished ones.  ``generate`` is the batch
+convenience the bench and the adapter use.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+from .config import ModelConfig
+
+
+@dataclass
+class Result:
+    tag: int
+    ids: list
+    finish: str  # "eos" | "length" | "error"
+    n_prompt: int
+
+
+_FINISH = {L.MS_FINISH_EOS: "eos", L.MS_FINISH_LENGTH: "length", L.MS_FINISH_ERROR: "error"}
+
+
+class Engine:
+    def __init__(self, cfg: ModelConfig, device: int = 0, max_batch: int = 8, max_ctx: int = 4096,
+                 max_prefill_tokens: int = 16384, n_pages: int = 0, eos_ids=None):
+        self.cfg = cfg
+        self.lib = L.load()
+        c = L.MsConfig()
+        c.abi_version = L.MS_ABI_VERSION
+        c.n_layers, c.hidden, c.n_heads = cfg.n_layers, cfg.hidden, cfg.n_heads
+        c.n_kv_heads, c.head_dim, c.ffn, c.vocab = cfg.n_kv_heads, cfg.head_dim, cfg.ffn, cfg.vocab
+        c.rope_theta, c.rope_factor = cfg.rope_theta, cfg.rope_factor
+        c.rope_low_freq_factor, c.rope_high_freq_factor = cfg.rope_low_freq_factor, cfg.rope_high_freq_factor
+        c.rope_orig_ctx, c.norm_eps = cfg.rope_orig_ctx, cfg.norm_eps
+        c.tie_embeddings = int(cfg.tie_embeddings)
+        c.device, c.max_batch, c.max_ctx = device, max_batch, max_ctx
+        c.max_prefill_tokens, c.n_pages = max_prefill_tokens, n_pages
+        eos = tuple(cfg.eos_ids if eos_ids is None else eos_ids)
+        if len(eos) > 8:
+            raise ValueError("at most 8 eos ids")
+        c.n_eos = len(eos)
+        for i, t in enumerate(eos):
+            c.eos_ids[i] = int(t)
+        h = C.c_void_p()
+        L.check(self.lib.ms_create(C.byref(c), C.byref(h)), None, "ms_create")
+        self.h = h
+        self.max_batch, self.max_ctx, self.max_prefill_tokens = max_batch, max_ctx, max_prefill_tokens
+        self._next_tag = 1
+
+    # ------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.ms_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _chk(self, rc, what):
+        return L.check(rc, self.h, what)
+
+    # ------------------------------------------------------------ weights
+    def init_synthetic(self, seed: int = 0, std: float = 0.02, norm_jitter: float = 0.0):
+        self._chk(self.lib.ms_init_synthetic(self.h, seed, std, norm_jitter), "ms_init_synthetic")
+
+    def load_tensor(self, tensor: int, layer: int, bf16_bits: np.ndarray):
+        a = np.ascontiguousarray(bf16_bits, dtype=np.uint16)
+        self._chk(self.lib.ms_load_weight(self.h, tensor, layer, a.ctypes.data, a.size), "ms_load_weight")
+
+    # ------------------------------------------------------------ request path
+    def submit(self, ids, num_predict: int, ignore_eos: bool = False, tag: int | None = None) -> int:
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        if tag is None:
+            tag = self._next_tag
+            self._next_tag += 1
+        flags = L.MS_FLAG_IGNORE_EOS if ignore_eos else 0
+        self._chk(self.lib.ms_submit(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size,
+                                     int(num_predict), flags, int(tag)), "ms_submit")
+        return tag
+
+    def step(self) -> int:
+        return self._chk(self.lib.ms_step(self.h), "ms_step")
+
+    def pending(self) -> int:
+        return self._chk(self.lib.ms_pending(self.h), "ms_pending")
+
+    def poll(self, cap: int = 256) -> list:
+        buf = (L.MsResult * cap)()
+        n = self._chk(self.lib.ms_poll(self.h, buf, cap), "ms_poll")
+        out = []
+        for i in range(n):
+            r = buf[i]
+            ids = [r.ids[j] for j in range(r.n_ids)] if r.n_ids else []
+            out.append(Result(int(r.tag), ids, _FINISH.get(r.finish_reason, "error"), int(r.n_prompt)))
+        return out
+
+    def generate(self, prompts, num_predict: int, ignore_eos: bool = False) -> list:
+        """Run every prompt (list of id lists) to completion; results in input order."""
+        tags = [self.submit(p, num_predict, ignore_eos) for p in prompts]
+        got = {}
+        while len(got) < len(tags):
+            pending = self.step()
+            for r in self.poll():
+                got[r.tag] = r
+            if pending == 0 and len(got) < len(tags):
+                for r in self.poll():
+                    got[r.tag] = r
+                if len(got) < len(tags):
+                    raise RuntimeError("engine drained without finishing every request")
+        return [got[t] for t in tags]
+
+    # ------------------------------------------------------------ probes / stats
+    def forward(self, ids, n_layers: int | None = None, hidden: bool = True, logits: bool = False):
+        cfg = self.cfg
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        n = a.size
+        nl = cfg.n_layers if n_layers is None else n_layers
+        hid = np.empty((n, cfg.hidden), np.float32) if hidden else None
+        lg = np.empty((n, cfg.vocab), np.float32) if logits else None
+        self._chk(self.lib.ms_forward(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)), n, nl,
+                                      hid.ctypes.data if hid is not None else None,
+                                      lg.ctypes.data if lg is not None else None), "ms_forward")
+        return hid, lg
+
+    def set_profiling(self, mask: int):
+        self._chk(self.lib.ms_set_profiling(self.h, mask), "ms_set_profiling")
+
+    def reset_stats(self):
+        self._chk(self.lib.ms_reset_stats(self.h), "ms_reset_stats")
+
+    def synchronize(self):
+        self._chk(self.lib.ms_synchronize(self.h), "ms_synchronize")
+
+    def stats(self) -> dict:
+        s = L.MsStats()
+        self._chk(self.lib.ms_get_stats(self.h, C.byref(s)), "ms_get_stats")
+        return {"prefill_tokens": s.prefill_tokens, "decode_tokens": s.decode_tokens,
+                "prefill_passes": s.prefill_passes, "decode_steps": s.decode_steps,
+                "finished": s.finished, "prefill_ms": s.prefill_ms, "decode_ms": s.decode_ms,
+                "kernel_ms": list(s.kernel_ms), "kernel_launches": list(s.kernel_launches)}

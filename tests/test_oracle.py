@@ -1,0 +1,86 @@
+"""CPU tests: the oracle pinned against its golden vectors (no GPU).
+
+tests/golden/hf_tiny_llama.npz holds transformers.LlamaForCausalLM outputs on the
+oracle's own seeded weights (tests/golden/make_golden.py).  In fp32 mode the oracle
+must reproduce them to fp32 round-off; in its bf16-rounding mode (the engine's
+numerics contract) within the north-star tolerance.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from mapsum.config import LLAMA32_3B, TINY
+from oracle import synth
+from oracle.llama_ref import OracleLlama, rope_inv_freq
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "hf_tiny_llama.npz")
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return np.load(GOLD, allow_pickle=False)
+
+
+@pytest.fixture(scope="module")
+def weights(gold):
+    return synth.make_weights(TINY, int(gold["seed"]), std=float(gold["std"]), jitter=float(gold["jitter"]))
+
+
+def test_oracle_fp32_matches_transformers(gold, weights):
+    o = OracleLlama(TINY, weights, round_bf16=False)
+    ids = gold["ids"]
+    lg, probes = o.forward(ids, collect=True, all_logits=True)
+    top_idx, top_val = gold["top16_idx"], gold["top16_val"]
+    mine = np.take_along_axis(lg, top_idx, 1)
+    assert np.allclose(mine, top_val, rtol=1e-4, atol=1e-4)
+    assert np.array_equal(np.argmax(lg, 1), top_idx[:, 0])
+    assert np.allclose(lg[-1], gold["last_logits"], rtol=1e-4, atol=1e-4)
+    for l in range(TINY.n_layers):
+        assert np.allclose(probes[l][:, :32], gold["hidden_head"][l], rtol=1e-4, atol=1e-4)
+        assert np.allclose(np.linalg.norm(probes[l], axis=1), gold["hidden_norm"][l], rtol=1e-5)
+
+
+def test_oracle_fp32_greedy_matches_transformers(gold, weights):
+    o = OracleLlama(TINY, weights, round_bf16=False)
+    toks, fin = o.generate(gold["ids"], len(gold["greedy"]), ignore_eos=True)
+    assert toks == gold["greedy"].tolist() and fin == "length"
+
+
+def test_oracle_bf16_mode_within_tolerance(gold, weights):
+    """The rounding points the HIP path implements stay within 2e-2 of fp32 Llama."""
+    o = OracleLlama(TINY, weights, round_bf16=True)
+    lg, _ = o.forward(gold["ids"])
+    ref = gold["last_logits"]
+    assert np.linalg.norm(lg - ref) / np.linalg.norm(ref) < 2e-2
+
+
+def test_llama3_rope_frequencies():
+    """Llama-3.2 rope_scaling: factor 32, low/high 1/4, original ctx 8192 (EXT config)."""
+    inv = rope_inv_freq(LLAMA32_3B)
+    base = 1.0 / (500000.0 ** (np.arange(0, 128, 2) / 128))
+    wl = 2 * np.pi / base
+    assert np.allclose(inv[wl < 2048], base[wl < 2048])          # high-frequency: untouched
+    assert np.allclose(inv[wl > 8192], base[wl > 8192] / 32.0)   # low-frequency: / factor
+    mid = (wl >= 2048) & (wl <= 8192)
+    assert np.all((inv[mid] <= base[mid]) & (inv[mid] >= base[mid] / 32.0))
+
+
+def test_synth_generator_known_answers():
+    """Pins the counter-based generator the engine restates on the device."""
+    assert int(synth.splitmix64(np.uint64(0))) == 0xE220A8397B1DCDAF  # published splitmix64(0)
+    w = synth.linear(0, synth.WQ, 3, 4, 8, 0.02)
+    assert w.dtype == np.float32 and w.shape == (4, 8)
+    assert np.array_equal(synth.bf16_rne(w), w)                  # already bf16 values
+    big = synth.linear(1, synth.EMBED, 0, 256, 256, 0.02)
+    assert abs(float(big.std()) - 0.02) < 0.001 and abs(float(big.mean())) < 0.001
+    g = synth.norm(1, synth.ATTN_NORM, 0, 1024, 0.0)
+    assert np.all(g == 1.0)
+
+
+def test_bf16_rounding_is_nearest_even():
+    x = np.array([1.0, 1.00390625, 1.01171875, -2.5, 3.0e38], np.float32)
+    r = synth.bf16_rne(x)
+    assert r.tolist()[:4] == [1.0, 1.0, 1.015625, -2.5]
+    bits = synth.to_bf16_bits(r)
+    assert np.array_equal(synth.from_bf16_bits(bits), r)
