@@ -157,6 +157,9 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* workspace, void* stream);
+/* tuning hook: as ms_op_gemv with the K-splitting wave count forced (0 = heuristic) */
+int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+                     int32_t ldo, int32_t epilogue, void* workspace, int32_t waves, void* stream);
 /* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
                   const int32_t* row_idx, void* stream);

@@ -161,7 +161,7 @@ struct ms_engine {
   void gemm_or_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, bool decode, int cls) {
     prof_begin(cls);
-    if (decode && M <= 64)
+    if (decode && gemv_supported(M, N, K, epi))
       launch_gemv(X, W, out, M, N, K, ldo, epi, gemv_ws, stream);
     else
       launch_gemm(X, W, out, M, N, K, ldo, epi, stream);
@@ -825,18 +825,23 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
 }
 
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K) {
-  if (M < 1 || M > 64 || N < 16 || K < 256 || K % 256) return MS_EINVAL;
+  if (M < 1 || M > 64 || N < 16 || K < 64 || K % 64) return MS_EINVAL;
   return (int64_t)gemv_workspace_bytes(M, N, K);
 }
 
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t ldo,
                int32_t epi, void* ws, void* stream) {
+  return ms_op_gemv_tuned(X, W, out, M, N, K, ldo, epi, ws, 0, stream);
+}
+
+int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+                     int32_t ldo, int32_t epi, void* ws, int32_t waves, void* stream) {
   return op_guard([&] {
-    REQUIRE(X && W && out && ws && M >= 1 && M <= 64 && N >= 16 && N % 16 == 0 && K >= 256 &&
-                K % 256 == 0,
-            MS_EINVAL, "bad gemv shape (M<=64, N%16==0, K%256==0)");
+    REQUIRE(X && W && out && ws && N >= 16 && N % 16 == 0, MS_EINVAL, "bad gemv operands");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
-    launch_gemv((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, ws, (hipStream_t)stream);
+    REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
+    launch_gemv_waves((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, waves,
+                      (hipStream_t)stream);
   });
 }
 

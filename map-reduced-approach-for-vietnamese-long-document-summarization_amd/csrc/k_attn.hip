@@ -191,10 +191,12 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 }
 
 // ============================================================ decode (split-K over keys)
-// grid (B, Hk, nsplit); block 256 = 4 waves; each wave owns pages of the split in
-// round robin and keeps its own online softmax for the G query heads of its kv head
-// (MFMA columns 0..G-1).  Partial (m, l, o[128]) per (b, q head, split) -> combine.
-constexpr int kSplitPages = 4;  // 256 keys per block
+// grid (B, Hk, nsplit); block 256 = 4 waves, ONE 64-key page per wave, so a block covers
+// 256 keys and every wave has its whole page (K as MFMA fragments + V rows, 32 KB)
+// in flight before its first MFMA.  The G query heads of the kv head are MFMA columns
+// 0..G-1.  Per-wave (m, l, O^T) are merged in LDS (reusing the wave's V image) and the
+// block writes one partial (m, l, o[128]) per (b, q head, split) for the combine kernel.
+constexpr int kSplitPages = 4;  // = waves per block
 
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
   const int nsplit = (max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
                                                           int Hk, KVView kv, DecodeAttnArgs a,
                                                           float* __restrict__ ws, int nsplit,
                                                           float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + 4 * 16 * 130 * 4];
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int b = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
@@ -214,41 +216,40 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   const int slot = a.seq_slot[b];
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
   char* vs_ = smem + wave * 16384;
-  float* mrg = (float*)(smem + 4 * 16384);  // [wave][16 cols][130] m, l, o[128]
+  const int pg = split * kSplitPages + wave;
+  const bool active = pg * kPage < len;  // wave-uniform
 
-  bf16x8 qf[4];
-  {
-    const int hq = kvh * G + min(r, G - 1);
-    const bf16_t* qrow = qkv + (size_t)b * row_stride + hq * kHeadDim;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
-  }
   f32x4 o[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
-  const int page_lo = split * kSplitPages;
-  const int npages = (len + kPage - 1) / kPage;
-  for (int pg = page_lo + wave; pg < min(page_lo + kSplitPages, npages); pg += 4) {
-    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
-    // V page -> this wave's LDS (rows past len zeroed)
+  if (active) {
+    const size_t base =
+        ((size_t)kv.block_table[(size_t)slot * kv.max_pages + pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+    // issue the whole page: K fragments (16 rows x 64 B per instruction) and V rows (1 KB)
+    u32x4 kf[4][4], vr[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int c = i * 64 + lane, row = c >> 4, ch = c & 15;
-      u32x4 v = *(const u32x4*)(kv.v + base + row * kHeadDim + ch * 8);
-      if (pg * kPage + row >= len) v = u32x4{0, 0, 0, 0};
-      *(u32x4*)(vs_ + v_swz(row, ch)) = v;
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        kf[mt][s] = *(const u32x4*)(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s + 8 * g);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      vr[i] = *(const u32x4*)(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
+    bf16x8 qf[4];
+    {
+      const int hq = kvh * G + min(r, G - 1);
+      const bf16_t* qrow = qkv + (size_t)b * row_stride + hq * kHeadDim;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
     }
-    // S^T = K . Q^T with K straight from HBM (16 rows x 64 B per wave-instruction)
     f32x4 sc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bf16_t* krow = kv.k + base + (mt * 16 + r) * kHeadDim + 8 * g;
 #pragma unroll
-      for (int s = 0; s < 4; ++s) sc[mt] = mfma16(as_bf16x8(*(const uint4*)(krow + 32 * s)), qf[s], sc[mt]);
+      for (int s = 0; s < 4; ++s) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s]), qf[s], sc[mt]);
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -262,24 +263,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = mx;  // finite: key pg*64 < len is always visible
     float rs = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - m_new);
+        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - mx);
         sc[mt][j] = p;
         rs += p;
       }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
+    l_run = rs;
+    // V rows -> this wave's LDS image (rows past len zeroed: no stale V in P.V)
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's V tile is in LDS
+    for (int i = 0; i < 16; ++i) {
+      const int row = i * 4 + (lane >> 4);
+      if (pg * kPage + row >= len) vr[i] = u32x4{0, 0, 0, 0};
+      *(u32x4*)(vs_ + v_swz(row, lane & 15)) = vr[i];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the V image is in LDS
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int kstep = 0; kstep < 2; ++kstep) {
@@ -287,11 +291,12 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
   }
-  // merge the 4 waves: each wave publishes (m, l, O^T) for its 16 columns
+  // publish (m, l, O^T) of this wave's 16 columns into its own LDS region
   {
-    float* mw = mrg + wave * 16 * 130;
+    float* mw = (float*)vs_;
     if (g == 0) { mw[r * 130 + 0] = m_run; mw[r * 130 + 1] = l_run; }
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt)
@@ -299,19 +304,18 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
       for (int j = 0; j < 4; ++j) mw[r * 130 + 2 + dt * 16 + 4 * g + j] = o[dt][j];
   }
   __syncthreads();
-  // threads: col c < G, d in [0,128): 2 d per thread over 256 threads -> G*128 outputs
   for (int idx = tid; idx < G * 130; idx += 256) {
     const int c = idx / 130, k = idx % 130;
     float M = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) M = fmaxf(M, mrg[(w * 16 + c) * 130]);
+    for (int w = 0; w < 4; ++w) M = fmaxf(M, ((const float*)(smem + w * 16384))[c * 130]);
     float acc = 0.f;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
-      const float mw = mrg[(w * 16 + c) * 130];
-      const float f = (mw == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(mw - M);
-      const float v = mrg[(w * 16 + c) * 130 + k];
-      acc += (k == 0) ? 0.f : f * v;
+      const float* mw = (const float*)(smem + w * 16384);
+      const float m_w = mw[c * 130];
+      const float f = (m_w == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_w - M);
+      acc += (k == 0) ? 0.f : f * mw[c * 130 + k];
     }
     const int hq = kvh * G + c;
     float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;

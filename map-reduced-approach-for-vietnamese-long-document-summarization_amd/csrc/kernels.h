@@ -42,10 +42,14 @@ void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream
 // out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, hipStream_t s);
-// M <= 64 decode variant; ws: fp32 split-K slabs + tickets (see gemv_workspace_bytes)
+// M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits
 size_t gemv_workspace_bytes(int M, int N, int K);
+bool gemv_supported(int M, int N, int K, int epi);
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, void* ws, hipStream_t s);
+// tuning hook: force the number of K-splitting waves per block (0 = heuristic)
+void launch_gemv_waves(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                       int epi, int force_waves, hipStream_t s);
 
 void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s);

@@ -26,7 +26,7 @@ EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
-    "ms_op_gemv", "ms_op_rmsnorm", "ms_op_argmax",
+    "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_rmsnorm", "ms_op_argmax",
 )
 
 
@@ -87,6 +87,7 @@ def load() -> C.CDLL:
         "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_workspace": (i64, [i32, i32, i32]),
         "ms_op_gemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
+        "ms_op_gemv_tuned": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp]),
         "ms_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, C.c_float, vp, vp]),
         "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
     }

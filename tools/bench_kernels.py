@@ -1,0 +1,99 @@
+"""Kernel micro-benchmarks through the C-ABI op entry points (GPU).
+
+    python tools/bench_kernels.py gemv [--m 8]
+    python tools/bench_kernels.py gemm
+
+Times each launch with HIP events on the launch stream (median of interleaved rounds),
+reports algorithmic GB/s (gemv: weight + activation bytes) or TFLOP/s (gemm).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "map-reduced-approach-for-vietnamese-long-document-summarization_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mapsum import _lib as L  # noqa: E402
+
+
+def timeit(fn, reps=20, rounds=5):
+    s = torch.cuda.current_stream()
+    res = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        res.append(e0.elapsed_time(e1) / reps)
+    return float(np.median(res))
+
+
+def bench_gemv(lib, M, shapes, waves_list):
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    # a 1 GB buffer swept between rounds keeps weights out of the 256 MB MALL
+    flush = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)
+    for name, N, K, epi in shapes:
+        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02 for _ in range(8)]
+        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
+                          dtype=torch.float32 if epi in (1, 3) else torch.bfloat16)
+        ldo = N if epi != 2 else N // 2
+        byts = N * K * 2 + M * K * 2 + out.numel() * out.element_size() * (2 if epi == 1 else 1)
+        line = f"{name:8s} N={N:6d} K={K:5d} M={M:3d} {byts/1e6:8.1f} MB |"
+        for wv in waves_list:
+            i = [0]
+
+            def fn():
+                W = Ws[i[0] % len(Ws)]
+                i[0] += 1
+                rc = lib.ms_op_gemv_tuned(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi,
+                                          ws.data_ptr(), wv, st)
+                if rc:
+                    raise RuntimeError(lib.ms_last_error(None))
+            try:
+                flush.zero_()
+                t = timeit(fn)
+                line += f" w{wv}: {t*1e3:7.1f}us {byts/t/1e6:6.0f}GB/s |"
+            except RuntimeError:
+                line += f" w{wv}: n/a |"
+        print(line, flush=True)
+
+
+def bench_gemm(lib):
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, M, N, K, epi in [("qkv", 16384, 5120, 3072, 0), ("o", 16384, 3072, 3072, 1),
+                               ("gu", 16384, 16384, 3072, 2), ("down", 16384, 3072, 8192, 1),
+                               ("sq4k", 4096, 4096, 4096, 0)]:
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        W = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
+                          dtype=torch.float32 if epi in (1, 3) else torch.bfloat16)
+        ldo = N if epi != 2 else N // 2
+
+        def fn():
+            lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st)
+        t = timeit(fn, reps=5, rounds=3)
+        print(f"gemm {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s", flush=True)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", choices=["gemv", "gemm"])
+    ap.add_argument("--m", type=int, default=8)
+    a = ap.parse_args()
+    lib = L.load()
+    if a.what == "gemv":
+        shapes = [("qkv", 5120, 3072, 0), ("o", 3072, 3072, 1), ("gu", 16384, 3072, 2),
+                  ("down", 3072, 8192, 1), ("lm_head", 128256, 3072, 3)]
+        bench_gemv(lib, a.m, shapes, [0, 6, 8, 12, 16])
+    else:
+        bench_gemm(lib)
