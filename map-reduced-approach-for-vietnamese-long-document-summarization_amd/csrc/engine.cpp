@@ -20,6 +20,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -105,6 +106,11 @@ struct ms_engine {
   std::vector<std::pair<int, int>> ev_pending;  // (class, start event index); end = start+1
   size_t ev_used = 0;
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  // decode steps replay a captured hipGraph per (batch rows, attention splits): the
+  // kernels' pointers and the step-argument layout depend on nothing else
+  std::map<std::pair<int, int>, hipGraphExec_t> decode_graphs;
+  bool use_graphs = true;
+  int32_t* ids_host = nullptr;  // pinned landing buffer for the next greedy ids
 
   template <class T>
   T* dalloc(size_t n, bool zero = false) {
@@ -168,9 +174,57 @@ struct ms_engine {
     prof_end(cls);
   }
 
+  // decode with fused epilogues: norm, QKV+RoPE+KV-scatter, attention(+combine), O(+res),
+  // norm, gate/up+SwiGLU, down(+res) -- 8 launches per layer instead of 9
+  bool fused_decode(int B) const {
+    return gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV) &&
+           gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
+           gemv_supported(B, H, Hq * D, MS_GEMV_EPI_ADD_F32) &&
+           gemv_supported(B, H, F, MS_GEMV_EPI_ADD_F32);
+  }
+
+  void run_layer_fused_decode(int l, int B, const int32_t* tok_pos, const int32_t* tok_slot,
+                              const DecodeAttnArgs& da) {
+    const Layer& Ly = layers[l];
+    KVView kv = kv_layer(l);
+    prof_begin(K_MISC);
+    launch_rmsnorm(x, Ly.attn_norm, xb, B, H, cfg.norm_eps, nullptr, stream);
+    prof_end(K_MISC);
+    GemvArgs ga{};
+    ga.tok_pos = tok_pos;
+    ga.tok_slot = tok_slot;
+    ga.cos_tab = cos_tab;
+    ga.sin_tab = sin_tab;
+    ga.kv = kv;
+    ga.Hq = Hq;
+    ga.Hk = Hk;
+    prof_begin(K_GEMV);
+    launch_gemv_ex(xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, 0, stream);
+    prof_end(K_GEMV);
+    prof_begin(K_ATTN_DECODE);
+    launch_attn_decode(qkv, attn, Hq, Hk, kv, da, attn_ws, stream);
+    prof_end(K_ATTN_DECODE);
+    prof_begin(K_GEMV);
+    launch_gemv_ex(attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_ADD_F32, nullptr, 0, stream);
+    prof_end(K_GEMV);
+    prof_begin(K_MISC);
+    launch_rmsnorm(x, Ly.ffn_norm, xb, B, H, cfg.norm_eps, nullptr, stream);
+    prof_end(K_MISC);
+    prof_begin(K_GEMV);
+    launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, 0, stream);
+    prof_end(K_GEMV);
+    prof_begin(K_GEMV);
+    launch_gemv_ex(hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_ADD_F32, nullptr, 0, stream);
+    prof_end(K_GEMV);
+  }
+
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
   void run_layer(int l, int T, bool decode, const int32_t* tok_pos, const int32_t* tok_slot,
                  const PrefillAttnArgs& pa, const DecodeAttnArgs& da) {
+    if (decode && fused_decode(T)) {
+      run_layer_fused_decode(l, T, tok_pos, tok_slot, da);
+      return;
+    }
     const Layer& Ly = layers[l];
     const int kc = decode ? K_GEMV : K_GEMM;
     prof_begin(K_MISC);
@@ -263,6 +317,7 @@ void validate_config(const ms_config& c) {
   REQUIRE(c.n_layers > 0 && c.n_heads > 0 && c.n_kv_heads > 0 && c.n_heads % c.n_kv_heads == 0,
           MS_EINVAL, "bad head/layer counts");
   REQUIRE(c.n_heads / c.n_kv_heads <= 16, MS_EINVAL, "GQA group must be <= 16");
+  REQUIRE(c.n_heads + c.n_kv_heads <= 64, MS_EINVAL, "at most 64 query+key heads");
   REQUIRE(c.hidden == c.n_heads * c.head_dim, MS_EINVAL, "hidden must equal n_heads*head_dim");
   REQUIRE(c.hidden % 256 == 0 && c.ffn % 256 == 0, MS_EINVAL, "hidden and ffn must be multiples of 256");
   REQUIRE(c.vocab % 16 == 0 && c.vocab > 0, MS_EINVAL, "vocab must be a multiple of 16");
@@ -344,6 +399,8 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&E.ids_host, cfg->max_batch * sizeof(int32_t), hipHostMallocDefault));
+    if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
     HIP_OK(hipDeviceSynchronize());
     return MS_OK;
   });
@@ -361,6 +418,8 @@ int ms_destroy(ms_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->args_h) (void)hipHostFree(e->args_h);
+  if (e->ids_host) (void)hipHostFree(e->ids_host);
+  for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
@@ -393,8 +452,8 @@ int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* 
       case MS_T_FINAL_NORM: dst = E.final_norm; rows = 1; cols = H; break;
       case MS_T_ATTN_NORM: dst = E.layers[layer].attn_norm; rows = 1; cols = H; break;
       case MS_T_FFN_NORM: dst = E.layers[layer].ffn_norm; rows = 1; cols = H; break;
-      case MS_T_WQ: dst = E.layers[layer].wqkv; rows = QD; cols = H; break;
-      case MS_T_WK: dst = E.layers[layer].wqkv; rows = KD; cols = H; add = QD; break;
+      case MS_T_WQ: dst = E.layers[layer].wqkv; rows = QD; cols = H; mul = 0; break;
+      case MS_T_WK: dst = E.layers[layer].wqkv; rows = KD; cols = H; mul = 0; add = QD; break;
       case MS_T_WV: dst = E.layers[layer].wqkv; rows = KD; cols = H; add = QD + KD; break;
       case MS_T_WO: dst = E.layers[layer].wo; rows = H; cols = QD; break;
       case MS_T_WGATE: dst = E.layers[layer].wgu; rows = E.F; cols = H; mul = 32; break;
@@ -436,8 +495,8 @@ int ms_init_synthetic(ms_engine* e, uint64_t seed, float std_, float jitter) {
       Layer& Ly = E.layers[l];
       launch_synth_norm(Ly.attn_norm, MS_T_ATTN_NORM, l, H, seed, jitter, s);
       launch_synth_norm(Ly.ffn_norm, MS_T_FFN_NORM, l, H, seed, jitter, s);
-      launch_synth_linear(Ly.wqkv, MS_T_WQ, l, QD, H, seed, std_, 16, 0, s);
-      launch_synth_linear(Ly.wqkv, MS_T_WK, l, KD, H, seed, std_, 16, QD, s);
+      launch_synth_linear(Ly.wqkv, MS_T_WQ, l, QD, H, seed, std_, 0, 0, s);  // rope-permuted rows
+      launch_synth_linear(Ly.wqkv, MS_T_WK, l, KD, H, seed, std_, 0, QD, s);
       launch_synth_linear(Ly.wqkv, MS_T_WV, l, KD, H, seed, std_, 16, QD + KD, s);
       launch_synth_linear(Ly.wo, MS_T_WO, l, H, QD, seed, std_, 16, 0, s);
       launch_synth_linear(Ly.wgu, MS_T_WGATE, l, E.F, H, seed, std_, 32, 0, s);
@@ -598,26 +657,9 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   HIP_OK(hipMemcpyAsync(first_ids->data(), E.ids_out_d, S * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
 }
 
-// one greedy decode step for every running sequence (B rows of one token each)
-static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int32_t>& next) {
-  const int B = (int)batch.size();
-  std::vector<int32_t> a;
-  a.reserve(8 * B);
-  int max_len = 0;
-  const size_t o_ids = a.size();
-  for (Seq* s : batch) a.push_back(s->out.back());
-  const size_t o_pos = a.size();
-  for (Seq* s : batch) a.push_back(s->len);
-  const size_t o_slot = a.size();
-  for (Seq* s : batch) a.push_back(s->slot);
-  const size_t o_len = a.size();
-  for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
-  int32_t* d = E.upload_args(a);
-  DecodeAttnArgs da;
-  da.seq_len = d + o_len;
-  da.seq_slot = d + o_slot;
-  da.B = B;
-  da.max_len = max_len;
+// kernels of one decode step (no host synchronisation: capturable into a hipGraph)
+static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& da) {
+  const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
   PrefillAttnArgs pa{};
   E.prof_begin(K_MISC);
   launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
@@ -630,9 +672,49 @@ static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int3
   E.prof_begin(K_MISC);
   launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
   E.prof_end(K_MISC);
+}
+
+// one greedy decode step for every running sequence (B rows of one token each)
+static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int32_t>& next) {
+  const int B = (int)batch.size();
+  std::vector<int32_t> a;
+  a.reserve(4 * B);
+  int max_len = 0;
+  for (Seq* s : batch) a.push_back(s->out.back());  // [0, B)   token ids
+  for (Seq* s : batch) a.push_back(s->len);         // [B, 2B)  positions
+  for (Seq* s : batch) a.push_back(s->slot);        // [2B, 3B) block-table rows
+  for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
+  HIP_OK(hipEventRecord(E.ev_a, E.stream));
+  int32_t* d = E.upload_args(a);
+  DecodeAttnArgs da;
+  da.seq_len = d + 3 * (size_t)B;
+  da.seq_slot = d + 2 * (size_t)B;
+  da.B = B;
+  // the split grid only depends on the longest sequence rounded up to 256 keys
+  da.max_len = ((max_len + 255) / 256) * 256;
+  if (E.use_graphs && E.prof_mask == 0) {
+    const auto key = std::make_pair(B, da.max_len);
+    auto it = E.decode_graphs.find(key);
+    if (it == E.decode_graphs.end()) {
+      hipGraph_t g = nullptr;
+      HIP_OK(hipStreamBeginCapture(E.stream, hipStreamCaptureModeRelaxed));
+      decode_body(E, B, d, da);
+      HIP_OK(hipStreamEndCapture(E.stream, &g));
+      hipGraphExec_t ex = nullptr;
+      HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+      HIP_OK(hipGraphDestroy(g));
+      it = E.decode_graphs.emplace(key, ex).first;
+    }
+    HIP_OK(hipGraphLaunch(it->second, E.stream));
+  } else {
+    decode_body(E, B, d, da);
+  }
   HIP_OK(hipGetLastError());
+  HIP_OK(hipEventRecord(E.ev_b, E.stream));
+  HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_out_d, B * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
   next.resize(B);
-  HIP_OK(hipMemcpyAsync(next.data(), E.ids_out_d, B * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
+  HIP_OK(hipStreamSynchronize(E.stream));
+  std::memcpy(next.data(), E.ids_host, B * sizeof(int32_t));
 }
 
 int ms_step(ms_engine* e) {
@@ -680,10 +762,7 @@ int ms_step(ms_engine* e) {
     for (size_t i0 = 0; i0 < batch.size(); i0 += 256) {
       std::vector<Seq*> sub(batch.begin() + i0, batch.begin() + std::min(batch.size(), i0 + 256));
       std::vector<int32_t> next;
-      HIP_OK(hipEventRecord(E.ev_a, E.stream));
-      decode_step(E, sub, next);
-      HIP_OK(hipEventRecord(E.ev_b, E.stream));
-      HIP_OK(hipStreamSynchronize(E.stream));
+      decode_step(E, sub, next);  // records ev_a/ev_b around its device work and syncs
       float ms_ = 0.f;
       HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
       E.stats.decode_ms += ms_;
@@ -840,8 +919,8 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(X && W && out && ws && N >= 16 && N % 16 == 0, MS_EINVAL, "bad gemv operands");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
-    launch_gemv_waves((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, waves,
-                      (hipStream_t)stream);
+    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
+                   (hipStream_t)stream);
   });
 }
 

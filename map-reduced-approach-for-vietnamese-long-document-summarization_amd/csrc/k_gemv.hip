@@ -3,20 +3,26 @@
 // Replaces ggml mul_mat at decode time: every decode step
 // multiplies the B <= 64 in-flight sequences' rows by every weight matrix once, so the
 // step is HBM-bound on the 6.4 GB of bf16 weights.  Design for that:
-//  * one block per 16*NT weight rows, the whole K range split over the block's WAVES
-//    waves (reduced through LDS) -- no cross-block split-K, so no fences or tickets;
+//  * one block per 16*NT weight rows, the whole K range split over the block's waves
+//    (reduced through LDS) -- no cross-block split-K, so no fences or tickets;
 //  * every wave issues the loads of its whole K slice (U steps of 64) before its
 //    first MFMA: W straight HBM -> VGPR (no LDS round trip, cdna_hip_programming.md
 //    §5 'GEMV / M <= 16'), 32 contiguous bytes per lane per step, so a wave-instruction
 //    pair covers 16 full 128-B lines; X (tiny, L2-resident) is staged once per block
-//    into LDS and read back as MFMA fragments;
+//    into LDS (row stride 2K+16 B: conflict-free fragment reads) while W is in flight;
 //  * v_mfma_f32_16x16x32_bf16 with the sequences as MFMA rows (M padded to 16*MT);
 //    both operands use the same permuted k order (lane group g holds k0+16g..+15),
-//    which leaves every dot product unchanged;
-//  * epilogues: bf16 store (QKV), fp32 residual add (O, down), SwiGLU on
-//    16-row-interleaved gate/up (W_gu), fp32 store (lm_head logits).
-// The result is deterministic and independent of the batch composition: a row's
-// sum order depends only on K and the launch shape chosen for (N, K).
+//    which leaves every dot product unchanged.
+// Fusions that remove whole launches from the decode step:
+//  * (RMSNorm stays a separate launch: recomputing it in each of the hundreds of blocks
+//    of a launch measured slower -- GU 19 -> 35 us, lm_head 142 -> 355 us at M = 8);
+//  * EPI_ROPE_KV (QKV): Q/K rows are uploaded rope-permuted (dims i and i+64 in one
+//    16-row tile), so the epilogue applies RoPE, writes Q for attention and scatters
+//    K/V into the paged cache;
+//  * bf16 store, fp32 residual add (O, down), SwiGLU on 16-row-interleaved gate/up,
+//    fp32 store (lm_head logits).
+// Results are deterministic and independent of the batch composition: a row's sum
+// order depends only on (N, K), never on M or on the other rows.
 #include "kernels.h"
 
 namespace ms {
@@ -25,11 +31,10 @@ struct GemvPlan {
   int MT, NT, waves, U, tiles;
 };
 
-// shape heuristic: U steps of 64 per wave, waves*U*64 == K
 static GemvPlan gemv_plan(int M, int N, int K, int epi, int force_waves = 0) {
   GemvPlan p;
   p.MT = (M + 15) / 16;
-  p.NT = (epi == 2) ? 2 : 1;
+  p.NT = (epi == MS_GEMV_EPI_SWIGLU) ? 2 : 1;
   p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
   const int steps = K / 64;
   int best_w = 0;
@@ -48,12 +53,12 @@ static GemvPlan gemv_plan(int M, int N, int K, int epi, int force_waves = 0) {
 
 size_t gemv_workspace_bytes(int, int, int) { return 256; }
 
-// staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew makes the 16 rows of a
-// fragment read land on different banks); X rows >= M alias row M-1 and are never stored.
-static size_t gemv_x_lds(int M, int K) { return (size_t)M * (2 * (size_t)K + 16); }
+constexpr size_t kMaxLds = 160 * 1024;
 
+// staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of a
+// fragment read on different banks); rows >= M alias row M-1 and are never stored.
 static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
-  const size_t xs = xlds ? gemv_x_lds(M, K) : 0;
+  size_t xs = xlds ? (size_t)M * (2 * (size_t)K + 16) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;  // per-wave partials
   return xs > red ? xs : red;
 }
@@ -64,11 +69,11 @@ template <int MT, int NT, int EPI, int U, bool XL>
 __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
-                                                    int ldo) {
+                                                    int ldo, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nthreads = blockDim.x;
+  const int nthreads = blockDim.x, nw = nthreads >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
   const int kbeg = wave * U * 64;
@@ -130,18 +135,59 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     for (int n = 0; n < NT; ++n)
       *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
   __syncthreads();
-  const int nw = nthreads >> 6;
-  // epilogue: element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
-  if constexpr (EPI == 2) {
+  // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
+  auto sum_e = [&](int e) {
+    float v = 0.f;
+    for (int q = 0; q < nw; ++q) v += red[q * ELEMS + e];
+    return v;
+  };
+  if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
     for (int e = tid; e < MT * 256; e += nthreads) {
       const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
       const int row = m * 16 + 4 * (l >> 4) + j;
       if (row >= M || n0 >= N) continue;
-      const int eg = ((m * NT + 0) * 64 + l) * 4 + j, eu = ((m * NT + 1) * 64 + l) * 4 + j;
-      float g = 0.f, u = 0.f;
-      for (int v = 0; v < nw; ++v) { g += red[v * ELEMS + eg]; u += red[v * ELEMS + eu]; }
+      const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j);
+      const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j);
       const int f = (n0 >> 5) * 16 + (l & 15);
       ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(g / (1.0f + __expf(-g)) * u);
+    }
+  } else if constexpr (EPI == MS_GEMV_EPI_ROPE_KV) {
+    static_assert(MT == 1 && NT == 1, "rope epilogue works on single 16-row tiles");
+    // element of (row, col) in tile (0, 0): l = 16*(row>>2) + col, j = row & 3
+    auto e_of = [](int row, int col) { return ((((row >> 2) << 4) + col) << 2) + (row & 3); };
+    const int QD = ga.Hq * kHeadDim, KD = ga.Hk * kHeadDim;
+    if (n0 < QD + KD) {  // Q or K head: tile t of head h holds dims 8t..8t+7 | 64+8t..64+8t+7
+      const bool is_q = n0 < QD;
+      const int h = is_q ? n0 / kHeadDim : (n0 - QD) / kHeadDim;
+      const int t = (n0 % kHeadDim) / 16;
+      for (int e = tid; e < M * 8; e += nthreads) {
+        const int row = e >> 3, c = e & 7, i = 8 * t + c;
+        const float lo = bf2f(f2bf(sum_e(e_of(row, c))));      // q/k rounded to bf16, then
+        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8))));  // rotated in fp32 (as prefill)
+        const int pos = ga.tok_pos[row];
+        const float cs = ga.cos_tab[(size_t)pos * 64 + i], sn = ga.sin_tab[(size_t)pos * 64 + i];
+        const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
+        const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
+        bf16_t* dst;
+        if (is_q) {
+          dst = (bf16_t*)out + (size_t)row * ldo + h * kHeadDim;
+        } else {
+          const int slot = ga.tok_slot[row];
+          const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
+          dst = ga.kv.k + (((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim;
+        }
+        dst[i] = f2bf(ra);
+        dst[64 + i] = f2bf(rb);
+      }
+    } else {  // V head: natural order, straight into the cache
+      const int h = (n0 - QD - KD) / kHeadDim, d0 = n0 % kHeadDim;
+      for (int e = tid; e < M * 16; e += nthreads) {
+        const int row = e >> 4, c = e & 15;
+        const int pos = ga.tok_pos[row], slot = ga.tok_slot[row];
+        const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
+        ga.kv.v[(((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim + d0 + c] =
+            f2bf(sum_e(e_of(row, c)));
+      }
     }
   } else {
     for (int e = tid; e < ELEMS; e += nthreads) {
@@ -150,81 +196,95 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       const int row = m * 16 + 4 * (l >> 4) + j;
       const int col = n0 + n * 16 + (l & 15);
       if (row >= M || col >= N) continue;
-      float v = 0.f;
-      for (int q = 0; q < nw; ++q) v += red[q * ELEMS + e];
+      const float v = sum_e(e);
       const size_t o = (size_t)row * ldo + col;
-      if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(v);
-      else if constexpr (EPI == 1) ((float*)out)[o] += v;
+      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v);
+      else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += v;
       else ((float*)out)[o] = v;
     }
   }
 }
 
-template <int MT, int NT, int U, bool XL>
-static void gemv_launch_x(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                          int epi, const GemvPlan& p, size_t lds, hipStream_t s) {
+template <int MT, int NT, int EPI, int U>
+static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                    const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+                    hipStream_t s) {
   const dim3 grid(p.tiles), blk(64 * p.waves);
-  if constexpr (NT == 2) {  // only SwiGLU runs on row pairs
-    hipLaunchKernelGGL((gemv_kernel<MT, 2, 2, U, XL>), grid, blk, lds, s, X, W, out, M, N, K, ldo);
+  if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
+    return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
-    switch (epi) {
-      case 0: hipLaunchKernelGGL((gemv_kernel<MT, 1, 0, U, XL>), grid, blk, lds, s, X, W, out, M, N, K, ldo); break;
-      case 1: hipLaunchKernelGGL((gemv_kernel<MT, 1, 1, U, XL>), grid, blk, lds, s, X, W, out, M, N, K, ldo); break;
-      default: hipLaunchKernelGGL((gemv_kernel<MT, 1, 3, U, XL>), grid, blk, lds, s, X, W, out, M, N, K, ldo); break;
-    }
+    if (xl)
+      hipLaunchKernelGGL((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M,
+                         N, K, ldo, ga);
+    else
+      hipLaunchKernelGGL((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out,
+                         M, N, K, ldo, ga);
   }
 }
 
-template <int MT, int NT, int U>
-static void gemv_launch_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                          int epi, const GemvPlan& p, size_t lds, bool xl, hipStream_t s) {
-  if (xl) gemv_launch_x<MT, NT, U, true>(X, W, out, M, N, K, ldo, epi, p, lds, s);
-  else gemv_launch_x<MT, NT, U, false>(X, W, out, M, N, K, ldo, epi, p, lds, s);
-}
-
-template <int MT, int NT>
-static void gemv_launch_mn(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                           int epi, const GemvPlan& p, size_t lds, bool xl, hipStream_t s) {
+template <int MT, int NT, int EPI>
+static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                      const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+                      hipStream_t s) {
+#define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldo, p, lds, xl, ga, s)
   switch (p.U) {
-    case 1: gemv_launch_u<MT, NT, 1>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 2: gemv_launch_u<MT, NT, 2>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 3: gemv_launch_u<MT, NT, 3>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 4: gemv_launch_u<MT, NT, 4>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 5: gemv_launch_u<MT, NT, 5>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 6: gemv_launch_u<MT, NT, 6>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    case 7: gemv_launch_u<MT, NT, 7>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
-    default: gemv_launch_u<MT, NT, 8>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s); break;
+    case 1: GU(1); break;
+    case 2: GU(2); break;
+    case 3: GU(3); break;
+    case 4: GU(4); break;
+    case 5: GU(5); break;
+    case 6: GU(6); break;
+    case 7: GU(7); break;
+    default: GU(8); break;
   }
+#undef GU
 }
 
-constexpr size_t kMaxLds = 160 * 1024;
+template <int MT>
+static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                       int epi, const GemvPlan& p, size_t lds, bool xl,
+                       const GemvArgs& ga, hipStream_t s) {
+#define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldo, p, lds, xl, ga, s)
+  switch (epi) {
+    case MS_GEMV_EPI_STORE_BF16: GE(1, MS_GEMV_EPI_STORE_BF16); break;
+    case MS_GEMV_EPI_ADD_F32: GE(1, MS_GEMV_EPI_ADD_F32); break;
+    case MS_GEMV_EPI_SWIGLU: GE(2, MS_GEMV_EPI_SWIGLU); break;
+    case MS_GEMV_EPI_ROPE_KV: GE(1, MS_GEMV_EPI_ROPE_KV); break;
+    default: GE(1, MS_GEMV_EPI_STORE_F32); break;
+  }
+#undef GE
+}
 
 bool gemv_supported(int M, int N, int K, int epi) {
   if (M < 1 || M > 64 || K % 64) return false;
+  if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
   const GemvPlan p = gemv_plan(M, N, K, epi);
-  return p.waves > 0 && gemv_lds_bytes(p, M, K, false) <= kMaxLds;
+  if (p.waves == 0) return false;
+  if (epi == MS_GEMV_EPI_ROPE_KV && gemv_lds_bytes(p, M, K, true) > kMaxLds) return false;
+  return gemv_lds_bytes(p, M, K, false) <= kMaxLds;
 }
 
-void launch_gemv_waves(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                       int epi, int force_waves, hipStream_t s) {
+void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                    int epi, const GemvArgs* ga_in, int force_waves, hipStream_t s) {
   if (M <= 0) return;
   const GemvPlan p = gemv_plan(M, N, K, epi, force_waves);
   if (p.waves == 0) return;  // callers check gemv_supported()
   const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
   const size_t lds = gemv_lds_bytes(p, M, K, xl);
   if (lds > kMaxLds) return;
-#define GV(MT_, NT_) gemv_launch_mn<MT_, NT_>(X, W, out, M, N, K, ldo, epi, p, lds, xl, s)
-  if (p.NT == 2) {
-    switch (p.MT) { case 1: GV(1, 2); break; case 2: GV(2, 2); break; case 3: GV(3, 2); break; default: GV(4, 2); }
-  } else {
-    switch (p.MT) { case 1: GV(1, 1); break; case 2: GV(2, 1); break; case 3: GV(3, 1); break; default: GV(4, 1); }
+  GemvArgs ga{};
+  if (ga_in) ga = *ga_in;
+  switch (p.MT) {
+    case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
+    case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
+    case 3: gemv_go_mt<3>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
+    default: gemv_go_mt<4>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
   }
-#undef GV
 }
 
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  void*, hipStream_t s) {
-  launch_gemv_waves(X, W, out, M, N, K, ldo, epi, 0, s);
+  launch_gemv_ex(X, W, out, M, N, K, ldo, epi, nullptr, 0, s);
 }
 
 }  // namespace ms

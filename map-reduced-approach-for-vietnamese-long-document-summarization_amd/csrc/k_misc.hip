@@ -35,7 +35,8 @@ void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x,
 }
 
 // ---------------------------------------------------------------- RMSNorm
-// y = bf16( (x * rsqrt(mean(x^2) + eps)) * w ), one 256-thread block per row.
+// y = bf16( (x * rsqrt(mean(x^2) + eps)) * w ), one 256-thread block per row; the row is
+// read once (<= 8 float4 per thread kept in registers, H <= 8192).
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x,
                                                       const bf16_t* __restrict__ w,
                                                       bf16_t* __restrict__ y, int H, float eps,
@@ -44,10 +45,14 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
   const int r = blockIdx.x;
   const int src = row_idx ? row_idx[r] : r;
   const float* xr = x + (size_t)src * H;
+  const int n4 = H / 4;
+  float4 v[8];
   float ss = 0.f;
-  for (int c = threadIdx.x; c < H / 4; c += 256) {
-    float4 v = *(const float4*)(xr + c * 4);
-    ss += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = min(threadIdx.x + k * 256, n4 - 1);  // clamped, never predicated
+    v[k] = *(const float4*)(xr + c * 4);
+    if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
   }
   ss = wave_sum(ss);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
@@ -55,14 +60,16 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float rinv = 1.0f / sqrtf(tot / (float)H + eps);
   bf16_t* yr = y + (size_t)r * H;
-  for (int c = threadIdx.x; c < H / 4; c += 256) {
-    float4 v = *(const float4*)(xr + c * 4);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int c = threadIdx.x + k * 256;
+    if (c >= n4) break;
     uint2 wv = *(const uint2*)(w + c * 4);
     float g0 = __uint_as_float(wv.x << 16), g1 = __uint_as_float(wv.x & 0xFFFF0000u);
     float g2 = __uint_as_float(wv.y << 16), g3 = __uint_as_float(wv.y & 0xFFFF0000u);
     uint2 o;
-    o.x = pack2bf((v.x * rinv) * g0, (v.y * rinv) * g1);
-    o.y = pack2bf((v.z * rinv) * g2, (v.w * rinv) * g3);
+    o.x = pack2bf((v[k].x * rinv) * g0, (v[k].y * rinv) * g1);
+    o.y = pack2bf((v[k].z * rinv) * g2, (v[k].w * rinv) * g3);
     *(uint2*)(yr + c * 4) = o;
   }
 }
@@ -74,14 +81,17 @@ void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H,
 }
 
 // ---------------------------------------------------------------- RoPE + KV scatter
-// qkv row layout: [Q heads | K heads | V heads] x 128.  rotate-half pairs (i, i+64).
-// One block per token; a thread owns 4 consecutive pair indices of one head.
+// qkv row layout: [Q heads | K heads | V heads] x 128, Q/K heads rope-permuted (the fused
+// weight rows are uploaded in rope_perm order so a 16-row GEMV tile holds dims i and i+64).
+// rotate-half pairs (i, i+64).  One block per token; the token's Q|K part is staged in LDS
+// first because Q is rewritten in place in natural dim order.
 __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, int Hq, int Hk,
                                                       const int32_t* __restrict__ tok_pos,
                                                       const int32_t* __restrict__ tok_slot,
                                                       const float* __restrict__ cos_tab,
                                                       const float* __restrict__ sin_tab,
                                                       KVView kv) {
+  __shared__ __attribute__((aligned(16))) bf16_t st[64 * kHeadDim];  // <= 64 Q+K heads
   const int t = blockIdx.x;
   const int pos = tok_pos[t];
   const int slot = tok_slot[t];
@@ -89,15 +99,19 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
   const int off = pos % kPage;
   const int row_elems = (Hq + 2 * Hk) * kHeadDim;
   bf16_t* row = qkv + (size_t)t * row_elems;
+  const int qk_elems = (Hq + Hk) * kHeadDim;
+  for (int c = threadIdx.x; c < qk_elems / 8; c += blockDim.x)
+    *(uint4*)(st + c * 8) = *(const uint4*)(row + c * 8);
+  __syncthreads();
   const int items = (Hq + 2 * Hk) * 16;
   for (int it = threadIdx.x; it < items; it += blockDim.x) {
     const int head = it >> 4;
-    const int i0 = (it & 15) * 4;
-    bf16_t* hp = row + head * kHeadDim;
-    uint2 lo = *(const uint2*)(hp + i0);
-    uint2 hi = *(const uint2*)(hp + i0 + 64);
-    uint2 olo = lo, ohi = hi;
-    if (head < Hq + Hk) {  // Q or K: rotate
+    const int i0 = (it & 15) * 4;  // dims i0..i0+3 and 64+i0..64+i0+3
+    uint2 olo, ohi;
+    if (head < Hq + Hk) {  // Q or K: rotate (from the permuted staging copy)
+      const bf16_t* hp = st + head * kHeadDim;
+      const uint2 lo = *(const uint2*)(hp + rope_perm(i0));
+      const uint2 hi = *(const uint2*)(hp + rope_perm(64 + i0));
       const float4 c = *(const float4*)(cos_tab + (size_t)pos * 64 + i0);
       const float4 sn = *(const float4*)(sin_tab + (size_t)pos * 64 + i0);
       float a[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xFFFF0000u),
@@ -114,8 +128,13 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
       }
       olo.x = pack2bf(ra[0], ra[1]); olo.y = pack2bf(ra[2], ra[3]);
       ohi.x = pack2bf(rb[0], rb[1]); ohi.y = pack2bf(rb[2], rb[3]);
+    } else {  // V: natural order, copied as is
+      const bf16_t* hp = row + head * kHeadDim;
+      olo = *(const uint2*)(hp + i0);
+      ohi = *(const uint2*)(hp + i0 + 64);
     }
     if (head < Hq) {
+      bf16_t* hp = row + head * kHeadDim;
       *(uint2*)(hp + i0) = olo;
       *(uint2*)(hp + i0 + 64) = ohi;
     } else {
@@ -206,8 +225,7 @@ __global__ void synth_linear_kernel(bf16_t* dst, int kind, int layer, int rows, 
        e += (size_t)gridDim.x * blockDim.x) {
     const int r = (int)(e / cols), c = (int)(e % cols);
     const float v = __fmul_rn((float)limb_sum(seed_h, kind, layer, r, c), scale);
-    const size_t dr = (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
-    dst[dr * cols + c] = rne_bits(v);
+    dst[map_row(r, map_mul, map_add) * cols + c] = rne_bits(v);
   }
 }
 
@@ -244,7 +262,7 @@ void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, f
 __global__ void scatter_rows_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
                                     int rows, int cols, int map_mul, int map_add) {
   const int r = blockIdx.x;
-  const size_t dr = (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
+  const size_t dr = map_row(r, map_mul, map_add);
   for (int c = threadIdx.x; c < cols; c += blockDim.x) dst[dr * cols + c] = src[(size_t)r * cols + c];
 }
 

@@ -33,7 +33,8 @@ struct DecodeAttnArgs {
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
 void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
                     const int32_t* row_idx, hipStream_t s);
-// RoPE on Q (in place) and K; K,V scattered into the paged cache.
+// RoPE on Q (in place, rope-permuted -> natural dim order) and K; K,V scattered into the
+// paged cache.  Q/K heads arrive in the rope-permuted row order of the fused weights.
 void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
                     KVView kv, hipStream_t s);
@@ -42,14 +43,31 @@ void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream
 // out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, hipStream_t s);
-// M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits
+// M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
+// Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
+enum {
+  MS_GEMV_EPI_STORE_BF16 = 0,
+  MS_GEMV_EPI_ADD_F32 = 1,
+  MS_GEMV_EPI_SWIGLU = 2,
+  MS_GEMV_EPI_STORE_F32 = 3,
+  MS_GEMV_EPI_ROPE_KV = 4
+};
+struct GemvArgs {
+  // ROPE_KV epilogue: Q -> out[row][h*128..] (ld = ldo), K/V -> paged cache
+  const int32_t* tok_pos;
+  const int32_t* tok_slot;
+  const float* cos_tab;
+  const float* sin_tab;
+  KVView kv;
+  int Hq, Hk;
+};
 size_t gemv_workspace_bytes(int M, int N, int K);
 bool gemv_supported(int M, int N, int K, int epi);
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, void* ws, hipStream_t s);
-// tuning hook: force the number of K-splitting waves per block (0 = heuristic)
-void launch_gemv_waves(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                       int epi, int force_waves, hipStream_t s);
+// ga: prologue/epilogue arguments (or null); force_waves: tuning hook (0 = heuristic)
+void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                    int epi, const GemvArgs* ga, int force_waves, hipStream_t s);
 
 void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s);
@@ -58,6 +76,15 @@ void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView k
                         DecodeAttnArgs a, float* ws, hipStream_t s);
 
 // synthetic weights (oracle/synth.py restates this generator)
+// row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the
+// rope permutation dst_row = (r & ~127) + rope_perm(r & 127) + map_add
+__host__ __device__ inline int rope_perm(int i) {
+  return i < 64 ? 16 * (i >> 3) + (i & 7) : 16 * ((i - 64) >> 3) + 8 + ((i - 64) & 7);
+}
+__host__ __device__ inline size_t map_row(int r, int map_mul, int map_add) {
+  if (map_mul == 0) return (size_t)(r & ~127) + rope_perm(r & 127) + map_add;
+  return (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
+}
 void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
                          float std, int map_mul, int map_add, hipStream_t s);
 void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,

@@ -266,3 +266,23 @@ def test_errors_are_reported(dev):
             e.submit(np.zeros(0, np.int32), 4)
     finally:
         e.close()
+
+
+def test_unfused_decode_path_large_batch(oracle):
+    """B > 16 runs the unfused decode chain (RMSNorm kernel, plain GEMV, RoPE kernel);
+    it must agree with the oracle as the fused B <= 16 chain does."""
+    e = Engine(TINY, device=0, max_batch=20, max_ctx=256, max_prefill_tokens=4096)
+    try:
+        e.init_synthetic(SEED, STD, JITTER)
+        prompts = [_prompt(30 + 7 * i, 900 + i) for i in range(20)]
+        res = e.generate(prompts, num_predict=8, ignore_eos=True)
+        matched = 0
+        for p, r in zip(prompts, res):
+            ref, _ = oracle.generate(p, 8, ignore_eos=True)
+            k = 0
+            while k < 8 and r.ids[k] == ref[k]:
+                k += 1
+            matched += k
+        assert matched / (20 * 8) >= 0.97, matched
+    finally:
+        e.close()
