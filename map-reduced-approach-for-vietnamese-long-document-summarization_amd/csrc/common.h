@@ -1,5 +1,6 @@
 // common.h -- shared device helpers for the gfx950 (CDNA4) map-phase kernels.
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -12,6 +13,25 @@ typedef short i16x4 __attribute__((ext_vector_type(4)));
 #define LDS_AS __attribute__((address_space(3)))
 
 namespace ms {
+
+// Kernel-duration probe: when the engine's profiling mask selects a kernel class it points
+// g_prof at an event pair; the next MS_LAUNCH then goes through hipExtLaunchKernelGGL, which
+// timestamps exactly that dispatch (no extra stream commands between kernels).
+struct ProfEvents {
+  hipEvent_t start, stop;
+};
+extern thread_local ProfEvents* g_prof;
+
+#define MS_LAUNCH(K, G, B, L, S, ...)                                                       \
+  do {                                                                                      \
+    if (::ms::g_prof) {                                                                     \
+      hipExtLaunchKernelGGL(K, G, B, L, S, ::ms::g_prof->start, ::ms::g_prof->stop, 0,      \
+                            __VA_ARGS__);                                                   \
+      ::ms::g_prof = nullptr;                                                               \
+    } else {                                                                                \
+      hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                                       \
+    }                                                                                       \
+  } while (0)
 
 constexpr int kWave = 64;
 constexpr int kHeadDim = 128;

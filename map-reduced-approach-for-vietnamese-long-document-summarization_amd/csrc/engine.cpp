@@ -102,8 +102,7 @@ struct ms_engine {
   std::vector<std::unique_ptr<Seq>> done, polled;
   ms_stats stats{};
   uint32_t prof_mask = 0;
-  std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> ev_pending;  // (class, start event index); end = start+1
+  std::vector<std::pair<int, int>> ev_pending;  // (class, event pair index)
   size_t ev_used = 0;
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
   // decode steps replay a captured hipGraph per (batch rows, attention splits): the
@@ -126,27 +125,31 @@ struct ms_engine {
   }
 
   // ---- profiling brackets -------------------------------------------------
+  // prof_begin(cls) arms ms::g_prof with an event pair; the next kernel launch of the class
+  // records its own start/stop (hipExtLaunchKernelGGL), so timings match rocprofv3.
+  std::vector<ProfEvents> ev_pairs;
   void prof_begin(int cls) {
     if (!((prof_mask >> cls) & 1)) return;
-    if (ev_used + 2 > ev_pool.size()) {
+    if (ev_used >= ev_pairs.size()) {
       for (int i = 0; i < 64; ++i) {
-        hipEvent_t ev;
-        HIP_OK(hipEventCreate(&ev));
-        ev_pool.push_back(ev);
+        ProfEvents pe;
+        HIP_OK(hipEventCreate(&pe.start));
+        HIP_OK(hipEventCreate(&pe.stop));
+        ev_pairs.push_back(pe);
       }
     }
     ev_pending.push_back({cls, (int)ev_used});
-    HIP_OK(hipEventRecord(ev_pool[ev_used], stream));
-    ev_used += 2;
+    g_prof = &ev_pairs[ev_used];
+    ev_used += 1;
   }
   void prof_end(int cls) {
     if (!((prof_mask >> cls) & 1)) return;
-    HIP_OK(hipEventRecord(ev_pool[ev_pending.back().second + 1], stream));
+    g_prof = nullptr;
   }
   void prof_collect() {  // after a stream sync
     for (auto& pr : ev_pending) {
       float ms_ = 0.f;
-      HIP_OK(hipEventElapsedTime(&ms_, ev_pool[pr.second], ev_pool[pr.second + 1]));
+      HIP_OK(hipEventElapsedTime(&ms_, ev_pairs[pr.second].start, ev_pairs[pr.second].stop));
       stats.kernel_ms[pr.first] += ms_;
       stats.kernel_launches[pr.first] += 1;
     }
@@ -420,7 +423,10 @@ int ms_destroy(ms_engine* e) {
   if (e->args_h) (void)hipHostFree(e->args_h);
   if (e->ids_host) (void)hipHostFree(e->ids_host);
   for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second);
-  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  for (auto& pe : e->ev_pairs) {
+    (void)hipEventDestroy(pe.start);
+    (void)hipEventDestroy(pe.stop);
+  }
   if (e->ev_a) (void)hipEventDestroy(e->ev_a);
   if (e->ev_b) (void)hipEventDestroy(e->ev_b);
   if (e->stream) (void)hipStreamDestroy(e->stream);

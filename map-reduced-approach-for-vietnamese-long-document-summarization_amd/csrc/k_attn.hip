@@ -186,7 +186,7 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
                          PrefillAttnArgs a, hipStream_t s) {
   if (a.n_qblk <= 0) return;
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
-  hipLaunchKernelGGL(attn_prefill_kernel, dim3(a.n_qblk, Hq), dim3(256), 0, s, qkv, out, Hq, Hk,
+  MS_LAUNCH(attn_prefill_kernel, dim3(a.n_qblk, Hq), dim3(256), 0, s, qkv, out, Hq, Hk,
                      kv, a, scale_log2);
 }
 
@@ -347,9 +347,9 @@ void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView k
   if (a.B <= 0) return;
   const int nsplit = (a.max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(a.B, Hk, nsplit), dim3(256), 0, s, qkv, Hq, Hk, kv,
+  MS_LAUNCH(attn_decode_kernel, dim3(a.B, Hk, nsplit), dim3(256), 0, s, qkv, Hq, Hk, kv,
                      a, ws, nsplit, scale_log2);
-  hipLaunchKernelGGL(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq,
+  MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq,
                      nsplit);
 }
 

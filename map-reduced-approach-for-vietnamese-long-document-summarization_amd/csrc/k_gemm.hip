@@ -142,10 +142,10 @@ void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int 
   if (M <= 0) return;
   const int grid = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   switch (epi) {
-    case 0: hipLaunchKernelGGL(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    case 1: hipLaunchKernelGGL(gemm_kernel<1>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    case 2: hipLaunchKernelGGL(gemm_kernel<2>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    default: hipLaunchKernelGGL(gemm_kernel<3>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
+    case 0: MS_LAUNCH(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
+    case 1: MS_LAUNCH(gemm_kernel<1>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
+    case 2: MS_LAUNCH(gemm_kernel<2>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
+    default: MS_LAUNCH(gemm_kernel<3>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
   }
 }
 

@@ -214,10 +214,10 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
     if (xl)
-      hipLaunchKernelGGL((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M,
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M,
                          N, K, ldo, ga);
     else
-      hipLaunchKernelGGL((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out,
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out,
                          M, N, K, ldo, ga);
   }
 }

@@ -8,6 +8,8 @@
 
 namespace ms {
 
+thread_local ProfEvents* g_prof = nullptr;
+
 // ---------------------------------------------------------------- embedding
 // x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
@@ -31,7 +33,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
 
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
+  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
 }
 
 // ---------------------------------------------------------------- RMSNorm
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
 void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
                     const int32_t* row_idx, hipStream_t s) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, H, eps, row_idx);
+  MS_LAUNCH(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, H, eps, row_idx);
 }
 
 // ---------------------------------------------------------------- RoPE + KV scatter
@@ -152,7 +154,7 @@ void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
                     KVView kv, hipStream_t s) {
   if (T <= 0) return;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, s, qkv, Hq, Hk, tok_pos, tok_slot,
+  MS_LAUNCH(rope_kv_kernel, dim3(T), dim3(256), 0, s, qkv, Hq, Hk, tok_pos, tok_slot,
                      cos_tab, sin_tab, kv);
 }
 
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
 
 void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s) {
   if (rows <= 0) return;
-  hipLaunchKernelGGL(argmax_kernel, dim3(rows), dim3(1024), 0, s, logits, n, out);
+  MS_LAUNCH(argmax_kernel, dim3(rows), dim3(1024), 0, s, logits, n, out);
 }
 
 // ---------------------------------------------------------------- synthetic weights
@@ -248,14 +250,14 @@ void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, u
                          float std, int map_mul, int map_add, hipStream_t s) {
   // scale = float32(std*sqrt(3)/65536), computed in double then rounded once (as numpy does)
   const float scale = (float)((double)std * 1.7320508075688772 / 65536.0);
-  hipLaunchKernelGGL(synth_linear_kernel, dim3(2048), dim3(256), 0, s, dst, kind, layer, rows,
+  MS_LAUNCH(synth_linear_kernel, dim3(2048), dim3(256), 0, s, dst, kind, layer, rows,
                      cols, host_splitmix64(seed), scale, map_mul, map_add);
 }
 
 void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
                        hipStream_t s) {
   const float scale = (float)((double)jitter / 131070.0);
-  hipLaunchKernelGGL(synth_norm_kernel, dim3(16), dim3(256), 0, s, dst, kind, layer, n,
+  MS_LAUNCH(synth_norm_kernel, dim3(16), dim3(256), 0, s, dst, kind, layer, n,
                      host_splitmix64(seed), scale);
 }
 
@@ -268,7 +270,7 @@ __global__ void scatter_rows_kernel(const bf16_t* __restrict__ src, bf16_t* __re
 
 void launch_scatter_rows(const bf16_t* src, bf16_t* dst, int rows, int cols, int map_mul,
                          int map_add, hipStream_t s) {
-  hipLaunchKernelGGL(scatter_rows_kernel, dim3(rows), dim3(256), 0, s, src, dst, rows, cols,
+  MS_LAUNCH(scatter_rows_kernel, dim3(rows), dim3(256), 0, s, src, dst, rows, cols,
                      map_mul, map_add);
 }
 
