@@ -56,6 +56,29 @@ def gemv_bytes_per_step(cfg, B):
     return cfg.n_layers * (w + act)
 
 
+def _q4_k_m_bytes_per_weight(tensor, layer, n_layers):
+    """Device bytes per weight of one decode-GEMV operand under the Q4_K_M mix
+    (csrc/engine.cpp q4_k_m_type): Q4_K 144 B / 256, Q6_K repacked 224 B / 256."""
+    if tensor in ("wv", "w_down"):
+        more = layer < n_layers // 8 or layer >= 7 * n_layers // 8 or (layer - n_layers // 8) % 3 == 2
+        return 224 / 256 if more else 144 / 256
+    return 144 / 256
+
+
+def qgemv_bytes_per_step(cfg, B):
+    """gemv_bytes_per_step with K-quant weight bytes (BASELINE configs[4])."""
+    H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
+    qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
+    act = 2 * B * (H + qkv + cfg.n_heads * D + H + H + F + F + H) + 4 * B * H * 4
+    tot = 0.0
+    for l in range(cfg.n_layers):
+        bpw = lambda t: _q4_k_m_bytes_per_weight(t, l, cfg.n_layers)  # noqa: E731
+        tot += (bpw("wq") * (qkv - 2 * cfg.n_kv_heads * D) * H + bpw("wk") * cfg.n_kv_heads * D * H
+                + bpw("wv") * cfg.n_kv_heads * D * H + bpw("wo") * H * cfg.n_heads * D
+                + bpw("w_gate") * 2 * F * H + bpw("w_down") * H * F + act)
+    return tot
+
+
 def prefill_flops_per_chunk(cfg, P):
     """2*params_linear*P + lm_head on the last token + causal attention."""
     H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
@@ -121,6 +144,8 @@ def main():
     ap.add_argument("--prompt-len", type=int, default=2048)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--model", default="llama3.2-3b")
+    ap.add_argument("--weights", choices=("bf16", "q4_k_m"), default="bf16",
+                    help="q4_k_m = BASELINE configs[4]: random Q4_K/Q6_K blocks, K-quant decode GEMVs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip HIP-event timing of the GEMV class")
     args = ap.parse_args()
@@ -144,7 +169,11 @@ def main():
     max_ctx = args.prompt_len + args.gen_len
     eng = Engine(cfg, device=local_rank, max_batch=B, max_ctx=max_ctx,
                  max_prefill_tokens=B * args.prompt_len)
-    eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
+    quant = args.weights == "q4_k_m"
+    if quant:
+        eng.init_synthetic_q(seed=2, scale=0.02, norm_jitter=0.0)
+    else:
+        eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
     chunks = synthetic_chunks(B, args.prompt_len, doc=rank, vocab=cfg.vocab, bos=cfg.bos_id)
     units = [Unit(rank, i, args.prompt_len) for i in range(B)]
 
@@ -191,24 +220,27 @@ def main():
         launches = sp["kernel_launches"][L.K_GEMV]
         if launches:
             gemv_s = sp["kernel_ms"][L.K_GEMV] / 1e3
-            bytes_total = gemv_bytes_per_step(cfg, B) * sp["decode_steps"]
+            per_step = qgemv_bytes_per_step(cfg, B) if quant else gemv_bytes_per_step(cfg, B)
+            bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "gemv_kernel (decode QKV/O/gate-up/down projections)",
+                    "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
+                              + " decode QKV/O/gate-up/down projections)",
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
-                    "method": "HIP events per launch, one extra untimed map step"}
+                    "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}
     pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * B * args.steps
     out = {
         "metric": METRIC, "value": round(value, 4), "unit": "chunks/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-        "data": "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)",
-        "config": {"workload": f"configs[1]: {B} x {args.prompt_len}-tok chunks -> {args.gen_len}-tok "
+        "data": ("synthetic (random Q4_K/Q6_K blocks in the Q4_K_M mix, seed 2, uniform token ids)"
+                 if quant else "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)"),
+        "config": {"workload": f"{'configs[4]' if quant else 'configs[1]'}: {B} x {args.prompt_len}-tok chunks -> {args.gen_len}-tok "
                                f"greedy summaries per GPU (ignore_eos), batched prefill + decode, "
                                f"summary ids gathered to rank 0",
-                   "model": cfg.name, "chunks_per_gpu": B, "prompt_tokens": args.prompt_len,
+                   "model": cfg.name, "weights": args.weights, "chunks_per_gpu": B, "prompt_tokens": args.prompt_len,
                    "summary_tokens": args.gen_len, "global_batch": world * B,
                    "seq_len": args.prompt_len + args.gen_len, "parallelism": f"chunk-dp{world}"},
         "breakdown": {"prefill_ms_per_step": round(st["prefill_ms"] / args.steps, 2),

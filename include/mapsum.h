@@ -124,6 +124,17 @@ int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* 
 /* device-side counter-based N(0,std)-like init; restated in oracle/synth.py */
 int ms_init_synthetic(ms_engine* e, uint64_t seed, float std, float norm_jitter);
 
+/* ggml K-quant weights (Q4_K_M files: BASELINE.json config 5).  `blocks` are the tensor's
+ * rows as raw ggml blocks (Q4_K = 144 B, Q6_K = 210 B per 256 weights).  The engine keeps
+ * bf16(dequant) for prefill and the blocks for the dequant-fused decode GEMV.  RMSNorm
+ * weights stay bf16 (ms_load_weight). */
+#define MS_GGML_Q4_K 12
+#define MS_GGML_Q6_K 14
+int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggml_type,
+                     const void* host_blocks, int64_t n_bytes);
+/* random Q4_K/Q6_K blocks with the Q4_K_M per-tensor type mix (bench) */
+int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float norm_jitter);
+
 /* ---- request path (replaces one /api/generate per chunk) -------------------- */
 int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict,
               uint32_t flags, uint64_t tag);
@@ -160,6 +171,14 @@ int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, in
 /* tuning hook: as ms_op_gemv with the K-splitting wave count forced (0 = heuristic) */
 int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                      int32_t ldo, int32_t epilogue, void* workspace, int32_t waves, void* stream);
+/* K-quant ops: raw ggml blocks -> fp32 (bit-exact restatement of llama.cpp's
+   dequantize_row_q4_K/q6_K); raw rows -> bf16 rows + packed rows (Q6_K repacked to 224 B);
+   dequant-fused GEMV over packed rows (same epilogues as ms_op_gemv) */
+int ms_op_dequant(int32_t ggml_type, const void* blocks, int64_t n_blocks, float* out, void* stream);
+int ms_op_quant_rows(int32_t ggml_type, const void* blocks, int32_t rows, int32_t K, void* bf16_out,
+                     void* packed_out, void* stream);
+int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void* out, int32_t M,
+                int32_t N, int32_t K, int32_t ldo, int32_t epilogue, void* stream);
 /* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
                   const int32_t* row_idx, void* stream);

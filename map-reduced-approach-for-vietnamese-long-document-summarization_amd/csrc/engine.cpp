@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstring>
 #include <deque>
+#include <array>
 #include <functional>
 #include <map>
 #include <memory>
@@ -71,6 +72,15 @@ struct Layer {
          *wgu = nullptr, *wdown = nullptr;
 };
 
+// Quantised (ggml K-quant) copy of one fused matrix for the decode GEMV; `need` = the
+// logical tensors that must all be loaded quantised before decode uses it.
+struct QSlot {
+  QMat m{};
+  uint32_t loaded = 0, need = 0;
+  bool ready() const { return need != 0 && loaded == need; }
+};
+enum { QS_QKV = 0, QS_O = 1, QS_GU = 2, QS_DOWN = 3 };
+
 }  // namespace
 
 struct ms_engine {
@@ -81,6 +91,8 @@ struct ms_engine {
   int max_pages = 0, n_pages = 0, Tmax = 0;
   std::vector<void*> allocs;
   std::vector<Layer> layers;
+  std::vector<std::array<QSlot, 4>> lq;  // per layer: QKV, O, gate/up, down
+  QSlot lmq;                             // lm_head (the tied embedding when tie_embeddings)
   bf16_t *embed = nullptr, *final_norm = nullptr, *lm_head = nullptr;
   float *cos_tab = nullptr, *sin_tab = nullptr;
   bf16_t *kpool = nullptr, *vpool = nullptr;
@@ -177,6 +189,17 @@ struct ms_engine {
     prof_end(cls);
   }
 
+  // decode projection: the K-quant stream when that matrix was loaded quantised
+  void proj(const QSlot* q, const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K,
+            int ldo, int epi, const GemvArgs* ga, int cls) {
+    prof_begin(cls);
+    if (q && q->ready() && qgemv_supported(M, N, K, epi))
+      launch_qgemv(X, q->m, out, M, N, K, ldo, epi, ga, stream);
+    else
+      launch_gemv_ex(X, W, out, M, N, K, ldo, epi, ga, 0, stream);
+    prof_end(cls);
+  }
+
   // decode with fused epilogues: norm, QKV+RoPE+KV-scatter, attention(+combine), O(+res),
   // norm, gate/up+SwiGLU, down(+res) -- 8 launches per layer instead of 9
   bool fused_decode(int B) const {
@@ -201,24 +224,17 @@ struct ms_engine {
     ga.kv = kv;
     ga.Hq = Hq;
     ga.Hk = Hk;
-    prof_begin(K_GEMV);
-    launch_gemv_ex(xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, 0, stream);
-    prof_end(K_GEMV);
+    const auto& Q = lq[l];
+    proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
     prof_begin(K_ATTN_DECODE);
     launch_attn_decode(qkv, attn, Hq, Hk, kv, da, attn_ws, stream);
     prof_end(K_ATTN_DECODE);
-    prof_begin(K_GEMV);
-    launch_gemv_ex(attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_ADD_F32, nullptr, 0, stream);
-    prof_end(K_GEMV);
+    proj(&Q[QS_O], attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_ADD_F32, nullptr, K_GEMV);
     prof_begin(K_MISC);
     launch_rmsnorm(x, Ly.ffn_norm, xb, B, H, cfg.norm_eps, nullptr, stream);
     prof_end(K_MISC);
-    prof_begin(K_GEMV);
-    launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, 0, stream);
-    prof_end(K_GEMV);
-    prof_begin(K_GEMV);
-    launch_gemv_ex(hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_ADD_F32, nullptr, 0, stream);
-    prof_end(K_GEMV);
+    proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
+    proj(&Q[QS_DOWN], hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_ADD_F32, nullptr, K_GEMV);
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
@@ -361,6 +377,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.lm_head = cfg->tie_embeddings ? E.embed : E.dalloc<bf16_t>((size_t)E.V * E.H);
     E.final_norm = E.dalloc<bf16_t>(E.H);
     E.layers.resize(E.L);
+    E.lq.resize(E.L);
     for (auto& Ly : E.layers) {
       Ly.attn_norm = E.dalloc<bf16_t>(E.H);
       Ly.ffn_norm = E.dalloc<bf16_t>(E.H);
@@ -439,50 +456,192 @@ const char* ms_last_error(const ms_engine* e) {
   return g_last_error.c_str();
 }
 
+// where a logical tensor lives: fused bf16 destination + row map, and its K-quant slot
+struct TensorDst {
+  bf16_t* dst = nullptr;
+  int rows = 0, cols = 0, mul = 16, add = 0;
+  QSlot* qs = nullptr;
+  int qbit = 0, qneed = 0, qregion = 0, qrow0 = 0, qrows = 0;
+};
+
+static TensorDst tensor_dst(ms_engine& E, int tensor, int layer) {
+  const bool per_layer = tensor != MS_T_EMBED && tensor != MS_T_FINAL_NORM && tensor != MS_T_LM_HEAD;
+  REQUIRE(!per_layer || (layer >= 0 && layer < E.L), MS_EINVAL, "layer out of range");
+  const int H = E.H, QD = E.Hq * E.D, KD = E.Hk * E.D;
+  TensorDst t;
+  auto q = [&](QSlot* s, int bit, int need, int region, int row0, int rows) {
+    t.qs = s; t.qbit = bit; t.qneed = need; t.qregion = region; t.qrow0 = row0; t.qrows = rows;
+  };
+  switch (tensor) {
+    case MS_T_EMBED:
+      t.dst = E.embed; t.rows = E.V; t.cols = H;
+      if (E.cfg.tie_embeddings) q(&E.lmq, 1, 1, 0, 0, E.V);
+      break;
+    case MS_T_LM_HEAD:
+      REQUIRE(!E.cfg.tie_embeddings, MS_EINVAL, "lm_head is tied to the embedding");
+      t.dst = E.lm_head; t.rows = E.V; t.cols = H; q(&E.lmq, 1, 1, 0, 0, E.V); break;
+    case MS_T_FINAL_NORM: t.dst = E.final_norm; t.rows = 1; t.cols = H; break;
+    case MS_T_ATTN_NORM: t.dst = E.layers[layer].attn_norm; t.rows = 1; t.cols = H; break;
+    case MS_T_FFN_NORM: t.dst = E.layers[layer].ffn_norm; t.rows = 1; t.cols = H; break;
+    case MS_T_WQ:  // rope-permuted rows (map_mul 0)
+      t.dst = E.layers[layer].wqkv; t.rows = QD; t.cols = H; t.mul = 0;
+      q(&E.lq[layer][QS_QKV], 1, 7, 0, 0, QD); break;
+    case MS_T_WK:
+      t.dst = E.layers[layer].wqkv; t.rows = KD; t.cols = H; t.mul = 0; t.add = QD;
+      q(&E.lq[layer][QS_QKV], 2, 7, 1, QD, KD); break;
+    case MS_T_WV:
+      t.dst = E.layers[layer].wqkv; t.rows = KD; t.cols = H; t.add = QD + KD;
+      q(&E.lq[layer][QS_QKV], 4, 7, 2, QD + KD, KD); break;
+    case MS_T_WO:
+      t.dst = E.layers[layer].wo; t.rows = H; t.cols = QD; q(&E.lq[layer][QS_O], 1, 1, 0, 0, H); break;
+    case MS_T_WGATE:  // gate/up interleaved per 16 rows
+      t.dst = E.layers[layer].wgu; t.rows = E.F; t.cols = H; t.mul = 32;
+      q(&E.lq[layer][QS_GU], 1, 3, 0, 0, 2 * E.F); break;
+    case MS_T_WUP:
+      t.dst = E.layers[layer].wgu; t.rows = E.F; t.cols = H; t.mul = 32; t.add = 16;
+      q(&E.lq[layer][QS_GU], 2, 3, 0, 0, 2 * E.F); break;
+    case MS_T_WDOWN:
+      t.dst = E.layers[layer].wdown; t.rows = H; t.cols = E.F; q(&E.lq[layer][QS_DOWN], 1, 1, 0, 0, H); break;
+    default: throw MsError(MS_EINVAL, "unknown tensor id " + std::to_string(tensor));
+  }
+  return t;
+}
+
 int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host, int64_t n) {
   if (!e) return MS_EINVAL;
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     REQUIRE(host != nullptr, MS_EINVAL, "null weight buffer");
     HIP_OK(hipSetDevice(E.cfg.device));
-    const bool per_layer = tensor != MS_T_EMBED && tensor != MS_T_FINAL_NORM && tensor != MS_T_LM_HEAD;
-    REQUIRE(!per_layer || (layer >= 0 && layer < E.L), MS_EINVAL, "layer out of range");
-    bf16_t* dst = nullptr;
-    int rows = 0, cols = 0, mul = 16, add = 0;
-    const int H = E.H, QD = E.Hq * E.D, KD = E.Hk * E.D;
-    switch (tensor) {
-      case MS_T_EMBED: dst = E.embed; rows = E.V; cols = H; break;
-      case MS_T_LM_HEAD:
-        REQUIRE(!E.cfg.tie_embeddings, MS_EINVAL, "lm_head is tied to the embedding");
-        dst = E.lm_head; rows = E.V; cols = H; break;
-      case MS_T_FINAL_NORM: dst = E.final_norm; rows = 1; cols = H; break;
-      case MS_T_ATTN_NORM: dst = E.layers[layer].attn_norm; rows = 1; cols = H; break;
-      case MS_T_FFN_NORM: dst = E.layers[layer].ffn_norm; rows = 1; cols = H; break;
-      case MS_T_WQ: dst = E.layers[layer].wqkv; rows = QD; cols = H; mul = 0; break;
-      case MS_T_WK: dst = E.layers[layer].wqkv; rows = KD; cols = H; mul = 0; add = QD; break;
-      case MS_T_WV: dst = E.layers[layer].wqkv; rows = KD; cols = H; add = QD + KD; break;
-      case MS_T_WO: dst = E.layers[layer].wo; rows = H; cols = QD; break;
-      case MS_T_WGATE: dst = E.layers[layer].wgu; rows = E.F; cols = H; mul = 32; break;
-      case MS_T_WUP: dst = E.layers[layer].wgu; rows = E.F; cols = H; mul = 32; add = 16; break;
-      case MS_T_WDOWN: dst = E.layers[layer].wdown; rows = H; cols = E.F; break;
-      default: throw MsError(MS_EINVAL, "unknown tensor id " + std::to_string(tensor));
-    }
-    REQUIRE(n == (int64_t)rows * cols, MS_EINVAL,
-            "tensor " + std::to_string(tensor) + ": expected " + std::to_string((int64_t)rows * cols) +
+    TensorDst t = tensor_dst(E, tensor, layer);
+    REQUIRE(n == (int64_t)t.rows * t.cols, MS_EINVAL,
+            "tensor " + std::to_string(tensor) + ": expected " + std::to_string((int64_t)t.rows * t.cols) +
                 " elements, got " + std::to_string(n));
-    if (rows == 1) {
-      HIP_OK(hipMemcpy(dst, host, (size_t)n * 2, hipMemcpyHostToDevice));
+    if (t.qs) t.qs->loaded &= ~(uint32_t)t.qbit;  // a bf16 reload supersedes a quantised copy
+    if (t.rows == 1) {
+      HIP_OK(hipMemcpy(t.dst, host, (size_t)n * 2, hipMemcpyHostToDevice));
       return MS_OK;
     }
     void* tmp = nullptr;
     HIP_OK(hipMalloc(&tmp, (size_t)n * 2));
     hipError_t ce = hipMemcpy(tmp, host, (size_t)n * 2, hipMemcpyHostToDevice);
     if (ce == hipSuccess) {
-      launch_scatter_rows((const bf16_t*)tmp, dst, rows, cols, mul, add, E.stream);
+      launch_scatter_rows((const bf16_t*)tmp, t.dst, t.rows, t.cols, t.mul, t.add, E.stream);
       ce = hipStreamSynchronize(E.stream);
     }
     (void)hipFree(tmp);
     HIP_OK(ce);
+    return MS_OK;
+  });
+}
+
+static uint8_t* q_region(ms_engine& E, QSlot& s, int idx, int row0, int rows, int type, int K) {
+  const uint8_t** base = idx == 0 ? &s.m.base0 : idx == 1 ? &s.m.base1 : &s.m.base2;
+  int* rw0 = idx == 0 ? &s.m.row0_0 : idx == 1 ? &s.m.row0_1 : &s.m.row0_2;
+  int* ty = idx == 0 ? &s.m.type0 : idx == 1 ? &s.m.type1 : &s.m.type2;
+  int* rb = idx == 0 ? &s.m.row_bytes0 : idx == 1 ? &s.m.row_bytes1 : &s.m.row_bytes2;
+  if (*base) {
+    REQUIRE(*ty == type, MS_EINVAL, "tensors sharing a fused region (gate/up) need one quant type");
+    return (uint8_t*)*base;
+  }
+  const int rowb = (K / 256) * qblock_bytes(type, true);
+  uint8_t* p = E.dalloc<uint8_t>((size_t)rows * rowb);
+  *base = p; *rw0 = row0; *ty = type; *rb = rowb;
+  s.m.n = std::max(s.m.n, idx + 1);
+  return p;
+}
+
+// device-resident raw ggml blocks of one logical tensor -> bf16 copy + quantised copy
+static void load_quant(ms_engine& E, int tensor, int layer, int type, const uint8_t* dblocks) {
+  TensorDst t = tensor_dst(E, tensor, layer);
+  REQUIRE(t.rows > 1, MS_EINVAL, "RMSNorm weights are not quantised");
+  REQUIRE(t.cols % 256 == 0, MS_EINVAL, "K-quant tensors need cols % 256 == 0");
+  // an untied embedding is only gathered: its bf16 copy is all decode needs
+  uint8_t* q = t.qs ? q_region(E, *t.qs, t.qregion, t.qrow0, t.qrows, type, t.cols) : nullptr;
+  launch_quant_rows(type, dblocks, t.rows, t.cols, t.dst, t.mul, t.add, q, t.qrow0, E.stream);
+  HIP_OK(hipGetLastError());
+  if (t.qs) {
+    t.qs->loaded |= (uint32_t)t.qbit;
+    t.qs->need = (uint32_t)t.qneed;
+  }
+}
+
+int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t type, const void* host,
+                     int64_t n_bytes) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(host != nullptr, MS_EINVAL, "null block buffer");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K (12) or Q6_K (14)");
+    HIP_OK(hipSetDevice(E.cfg.device));
+    TensorDst t = tensor_dst(E, tensor, layer);
+    const int64_t want = (int64_t)t.rows * (t.cols / 256) * qblock_bytes(type, false);
+    REQUIRE(t.cols % 256 == 0 && n_bytes == want, MS_EINVAL,
+            "tensor " + std::to_string(tensor) + ": expected " + std::to_string(want) + " bytes of blocks");
+    void* tmp = nullptr;
+    HIP_OK(hipMalloc(&tmp, (size_t)n_bytes));
+    int rc = MS_OK;
+    try {
+      HIP_OK(hipMemcpy(tmp, host, (size_t)n_bytes, hipMemcpyHostToDevice));
+      load_quant(E, tensor, layer, type, (const uint8_t*)tmp);
+      HIP_OK(hipStreamSynchronize(E.stream));
+    } catch (...) {
+      (void)hipFree(tmp);
+      throw;
+    }
+    (void)hipFree(tmp);
+    return rc;
+  });
+}
+
+// Q4_K_M per-tensor mix (EXT llama.cpp; restated in oracle/quants.py q4_k_m_type)
+static int q4_k_m_type(int tensor, int layer, int n_layers) {
+  if (tensor == MS_T_EMBED || tensor == MS_T_LM_HEAD) return MS_QT_Q6_K;
+  if (tensor == MS_T_WV || tensor == MS_T_WDOWN) {
+    const bool more = layer < n_layers / 8 || layer >= 7 * n_layers / 8 ||
+                      (layer - n_layers / 8) % 3 == 2;
+    return more ? MS_QT_Q6_K : MS_QT_Q4_K;
+  }
+  return MS_QT_Q4_K;
+}
+
+int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float jitter) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    HIP_OK(hipSetDevice(E.cfg.device));
+    hipStream_t s = E.stream;
+    size_t maxb = 0;
+    const int mats[] = {MS_T_WQ, MS_T_WK, MS_T_WV, MS_T_WO, MS_T_WGATE, MS_T_WUP, MS_T_WDOWN};
+    for (int tsr : mats) {
+      TensorDst t = tensor_dst(E, tsr, 0);
+      maxb = std::max(maxb, (size_t)t.rows * (t.cols / 256) * kQ6KBytes);
+    }
+    maxb = std::max(maxb, (size_t)E.V * (E.H / 256) * kQ6KBytes);
+    void* tmp = nullptr;
+    HIP_OK(hipMalloc(&tmp, maxb));
+    try {
+      auto one = [&](int tsr, int l) {
+        TensorDst t = tensor_dst(E, tsr, l);
+        const int ty = q4_k_m_type(tsr, l, E.L);
+        launch_synth_qblocks(ty, (uint8_t*)tmp, (int64_t)t.rows * (t.cols / 256),
+                             seed ^ ((uint64_t)tsr << 56) ^ ((uint64_t)l << 48), scale, s);
+        load_quant(E, tsr, l, ty, (const uint8_t*)tmp);
+      };
+      one(E.cfg.tie_embeddings ? MS_T_EMBED : MS_T_LM_HEAD, 0);
+      if (!E.cfg.tie_embeddings) one(MS_T_EMBED, 0);
+      launch_synth_norm(E.final_norm, MS_T_FINAL_NORM, 0, E.H, seed, jitter, s);
+      for (int l = 0; l < E.L; ++l) {
+        launch_synth_norm(E.layers[l].attn_norm, MS_T_ATTN_NORM, l, E.H, seed, jitter, s);
+        launch_synth_norm(E.layers[l].ffn_norm, MS_T_FFN_NORM, l, E.H, seed, jitter, s);
+        for (int tsr : mats) one(tsr, l);
+      }
+      HIP_OK(hipStreamSynchronize(s));
+    } catch (...) {
+      (void)hipFree(tmp);
+      throw;
+    }
+    (void)hipFree(tmp);
     return MS_OK;
   });
 }
@@ -674,7 +833,10 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   E.prof_begin(K_MISC);
   launch_rmsnorm(E.x, E.final_norm, E.xb, B, E.H, E.cfg.norm_eps, nullptr, E.stream);
   E.prof_end(K_MISC);
-  E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
+  if (E.lmq.ready() && qgemv_supported(B, E.V, E.H, MS_GEMV_EPI_STORE_F32))
+    E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_GEMV_EPI_STORE_F32, nullptr, K_LMHEAD);
+  else
+    E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
   E.prof_begin(K_MISC);
   launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
   E.prof_end(K_MISC);
@@ -927,6 +1089,41 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
     launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
                    (hipStream_t)stream);
+  });
+}
+
+int ms_op_dequant(int32_t type, const void* blocks, int64_t n_blocks, float* out, void* stream) {
+  return op_guard([&] {
+    REQUIRE(blocks && out && n_blocks >= 1, MS_EINVAL, "bad dequant arguments");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    launch_dequant_f32(type, (const uint8_t*)blocks, n_blocks, out, (hipStream_t)stream);
+  });
+}
+
+int ms_op_quant_rows(int32_t type, const void* blocks, int32_t rows, int32_t K, void* bf16_out,
+                     void* packed_out, void* stream) {
+  return op_guard([&] {
+    REQUIRE(blocks && bf16_out && rows >= 1 && K >= 256 && K % 256 == 0, MS_EINVAL, "bad quant_rows arguments");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    launch_quant_rows(type, (const uint8_t*)blocks, rows, K, (bf16_t*)bf16_out, 16, 0,
+                      (uint8_t*)packed_out, 0, (hipStream_t)stream);
+  });
+}
+
+int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int32_t M, int32_t N,
+                int32_t K, int32_t ldo, int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && packed && out && N >= 16, MS_EINVAL, "bad qgemv operands");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    REQUIRE(qgemv_supported(M, N, K, epi), MS_EINVAL, "qgemv shape unsupported (M<=64, K%256==0, N%16==0)");
+    QMat q{};
+    q.n = 1;
+    q.base0 = (const uint8_t*)packed;
+    q.row0_0 = 0;
+    q.type0 = type;
+    q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
+    launch_qgemv((const bf16_t*)X, q, out, M, N, K, ldo, epi, nullptr, (hipStream_t)stream);
   });
 }
 

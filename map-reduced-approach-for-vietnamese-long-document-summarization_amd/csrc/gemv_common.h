@@ -1,0 +1,107 @@
+// gemv_common.h -- pieces shared by the bf16 and the K-quant decode GEMVs.
+#pragma once
+#include "kernels.h"
+
+namespace ms {
+
+__device__ __forceinline__ uint4 ldg16(const void* p) { return *(const uint4*)p; }
+
+// X rows [M][K] bf16 -> LDS, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of an
+// MFMA fragment read on different banks).  Caller synchronises.
+__device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restrict__ X, int M, int K) {
+  const size_t xstride = 2 * (size_t)K + 16;
+  const int kch = K / 8;  // 16-B chunks per row
+  for (int c = threadIdx.x; c < M * kch; c += blockDim.x) {
+    const int r = c / kch, k8 = c - r * kch;
+    *(uint4*)(smem + r * xstride + k8 * 16) = ldg16(X + (size_t)r * K + k8 * 8);
+  }
+}
+
+// Cross-wave reduction of the per-wave MFMA accumulators through LDS and the epilogue.
+// acc[m][n][j] = C[row m*16 + 4*(lane>>4) + j][col n0 + n*16 + (lane&15)].
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, int M, int N,
+                                            int ldo, void* __restrict__ out, int n0,
+                                            const GemvArgs& ga) {
+  constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x, nw = nthreads >> 6;
+  __syncthreads();  // X image no longer needed: reuse LDS for the partials
+  float* red = (float*)smem;
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
+      *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
+  __syncthreads();
+  // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
+  auto sum_e = [&](int e) {
+    float v = 0.f;
+    for (int q = 0; q < nw; ++q) v += red[q * ELEMS + e];
+    return v;
+  };
+  if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
+    for (int e = tid; e < MT * 256; e += nthreads) {
+      const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
+      const int row = m * 16 + 4 * (l >> 4) + j;
+      if (row >= M || n0 >= N) continue;
+      const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j);
+      const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j);
+      const int f = (n0 >> 5) * 16 + (l & 15);
+      ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(g / (1.0f + __expf(-g)) * u);
+    }
+  } else if constexpr (EPI == MS_GEMV_EPI_ROPE_KV) {
+    static_assert(MT == 1 && NT == 1, "rope epilogue works on single 16-row tiles");
+    // element of (row, col) in tile (0, 0): l = 16*(row>>2) + col, j = row & 3
+    auto e_of = [](int row, int col) { return ((((row >> 2) << 4) + col) << 2) + (row & 3); };
+    const int QD = ga.Hq * kHeadDim, KD = ga.Hk * kHeadDim;
+    if (n0 < QD + KD) {  // Q or K head: tile t of head h holds dims 8t..8t+7 | 64+8t..64+8t+7
+      const bool is_q = n0 < QD;
+      const int h = is_q ? n0 / kHeadDim : (n0 - QD) / kHeadDim;
+      const int t = (n0 % kHeadDim) / 16;
+      for (int e = tid; e < M * 8; e += nthreads) {
+        const int row = e >> 3, c = e & 7, i = 8 * t + c;
+        const float lo = bf2f(f2bf(sum_e(e_of(row, c))));      // q/k rounded to bf16, then
+        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8))));  // rotated in fp32 (as prefill)
+        const int pos = ga.tok_pos[row];
+        const float cs = ga.cos_tab[(size_t)pos * 64 + i], sn = ga.sin_tab[(size_t)pos * 64 + i];
+        const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
+        const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
+        bf16_t* dst;
+        if (is_q) {
+          dst = (bf16_t*)out + (size_t)row * ldo + h * kHeadDim;
+        } else {
+          const int slot = ga.tok_slot[row];
+          const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
+          dst = ga.kv.k + (((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim;
+        }
+        dst[i] = f2bf(ra);
+        dst[64 + i] = f2bf(rb);
+      }
+    } else {  // V head: natural order, straight into the cache
+      const int h = (n0 - QD - KD) / kHeadDim, d0 = n0 % kHeadDim;
+      for (int e = tid; e < M * 16; e += nthreads) {
+        const int row = e >> 4, c = e & 15;
+        const int pos = ga.tok_pos[row], slot = ga.tok_slot[row];
+        const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
+        ga.kv.v[(((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim + d0 + c] =
+            f2bf(sum_e(e_of(row, c)));
+      }
+    }
+  } else {
+    for (int e = tid; e < ELEMS; e += nthreads) {
+      const int mn = e >> 8, l = (e >> 2) & 63, j = e & 3;
+      const int m = mn / NT, n = mn % NT;
+      const int row = m * 16 + 4 * (l >> 4) + j;
+      const int col = n0 + n * 16 + (l & 15);
+      if (row >= M || col >= N) continue;
+      const float v = sum_e(e);
+      const size_t o = (size_t)row * ldo + col;
+      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v);
+      else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += v;
+      else ((float*)out)[o] = v;
+    }
+  }
+}
+
+}  // namespace ms

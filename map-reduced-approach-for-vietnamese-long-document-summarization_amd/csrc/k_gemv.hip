@@ -23,7 +23,7 @@
 //    fp32 store (lm_head logits).
 // Results are deterministic and independent of the batch composition: a row's sum
 // order depends only on (N, K), never on M or on the other rows.
-#include "kernels.h"
+#include "gemv_common.h"
 
 namespace ms {
 
@@ -63,17 +63,13 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
   return xs > red ? xs : red;
 }
 
-__device__ __forceinline__ uint4 ldg16(const bf16_t* p) { return *(const uint4*)p; }
-
 template <int MT, int NT, int EPI, int U, bool XL>
 __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
                                                     int ldo, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nthreads = blockDim.x, nw = nthreads >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
   const int kbeg = wave * U * 64;
@@ -92,11 +88,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
   // 2. stage the M rows of X into LDS (XL) -- or read fragments from L2 (large M*K)
   const size_t xstride = 2 * (size_t)K + 16;
   if constexpr (XL) {
-    const int kch = K / 8;  // 16-B chunks per row
-    for (int c = tid; c < M * kch; c += nthreads) {
-      const int r = c / kch, k8 = c - r * kch;
-      *(uint4*)(smem + r * xstride + k8 * 16) = ldg16(X + (size_t)r * K + k8 * 8);
-    }
+    gemv_stage_x(smem, X, M, K);
     __syncthreads();
   }
 
@@ -127,82 +119,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       }
     }
   }
-  __syncthreads();  // X image no longer needed: reuse LDS for the partials
-  float* red = (float*)smem;
-#pragma unroll
-  for (int m = 0; m < MT; ++m)
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-      *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
-  __syncthreads();
-  // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
-  auto sum_e = [&](int e) {
-    float v = 0.f;
-    for (int q = 0; q < nw; ++q) v += red[q * ELEMS + e];
-    return v;
-  };
-  if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
-    for (int e = tid; e < MT * 256; e += nthreads) {
-      const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
-      const int row = m * 16 + 4 * (l >> 4) + j;
-      if (row >= M || n0 >= N) continue;
-      const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j);
-      const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j);
-      const int f = (n0 >> 5) * 16 + (l & 15);
-      ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(g / (1.0f + __expf(-g)) * u);
-    }
-  } else if constexpr (EPI == MS_GEMV_EPI_ROPE_KV) {
-    static_assert(MT == 1 && NT == 1, "rope epilogue works on single 16-row tiles");
-    // element of (row, col) in tile (0, 0): l = 16*(row>>2) + col, j = row & 3
-    auto e_of = [](int row, int col) { return ((((row >> 2) << 4) + col) << 2) + (row & 3); };
-    const int QD = ga.Hq * kHeadDim, KD = ga.Hk * kHeadDim;
-    if (n0 < QD + KD) {  // Q or K head: tile t of head h holds dims 8t..8t+7 | 64+8t..64+8t+7
-      const bool is_q = n0 < QD;
-      const int h = is_q ? n0 / kHeadDim : (n0 - QD) / kHeadDim;
-      const int t = (n0 % kHeadDim) / 16;
-      for (int e = tid; e < M * 8; e += nthreads) {
-        const int row = e >> 3, c = e & 7, i = 8 * t + c;
-        const float lo = bf2f(f2bf(sum_e(e_of(row, c))));      // q/k rounded to bf16, then
-        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8))));  // rotated in fp32 (as prefill)
-        const int pos = ga.tok_pos[row];
-        const float cs = ga.cos_tab[(size_t)pos * 64 + i], sn = ga.sin_tab[(size_t)pos * 64 + i];
-        const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
-        const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
-        bf16_t* dst;
-        if (is_q) {
-          dst = (bf16_t*)out + (size_t)row * ldo + h * kHeadDim;
-        } else {
-          const int slot = ga.tok_slot[row];
-          const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
-          dst = ga.kv.k + (((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim;
-        }
-        dst[i] = f2bf(ra);
-        dst[64 + i] = f2bf(rb);
-      }
-    } else {  // V head: natural order, straight into the cache
-      const int h = (n0 - QD - KD) / kHeadDim, d0 = n0 % kHeadDim;
-      for (int e = tid; e < M * 16; e += nthreads) {
-        const int row = e >> 4, c = e & 15;
-        const int pos = ga.tok_pos[row], slot = ga.tok_slot[row];
-        const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
-        ga.kv.v[(((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim + d0 + c] =
-            f2bf(sum_e(e_of(row, c)));
-      }
-    }
-  } else {
-    for (int e = tid; e < ELEMS; e += nthreads) {
-      const int mn = e >> 8, l = (e >> 2) & 63, j = e & 3;
-      const int m = mn / NT, n = mn % NT;
-      const int row = m * 16 + 4 * (l >> 4) + j;
-      const int col = n0 + n * 16 + (l & 15);
-      if (row >= M || col >= N) continue;
-      const float v = sum_e(e);
-      const size_t o = (size_t)row * ldo + col;
-      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v);
-      else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += v;
-      else ((float*)out)[o] = v;
-    }
-  }
+  gemv_finish<MT, NT, EPI>(acc, smem, M, N, ldo, out, n0, ga);
 }
 
 template <int MT, int NT, int EPI, int U>

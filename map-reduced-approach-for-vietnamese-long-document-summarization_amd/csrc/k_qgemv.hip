@@ -1,0 +1,358 @@
+// k_qgemv.hip -- ggml K-quant weights on gfx950: bit-exact dequantisation and the
+// dequant-fused decode GEMV (BASELINE.json config 5).
+//
+// Ollama's default llama3.2:3b is Q4_K_M: Q4_K (144 B / 256 weights) for most matrices,
+// Q6_K (210 B / 256 weights) for some (EXT: llama.cpp).  The dequantisers restate
+// llama.cpp's dequantize_row_q4_K / _q6_K (oracle/ggml_quants.c) with the non-contracted
+// float forms  y = d1*q - m1  and  y = (d*sc)*q  (__fmul_rn/__fsub_rn), so the fp32 result
+// is bit-identical to the C restatement.
+//
+// Storage (engine.cpp): every quantised matrix keeps both
+//   * a bf16 copy = bf16_rne(dequant(blocks)) in the fused row layout, for prefill GEMMs
+//     and the embedding gather (compute-bound; bf16 is what MFMA consumes), and
+//   * the quantised rows for decode, which is HBM-bound: 4.5 / 6.56 bits per weight
+//     instead of 16.  Q4_K rows keep the ggml block layout (144 B = 9 x 16 B, aligned);
+//     Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales 16 | d 2 + pad] so every
+//     field is 16-B aligned.
+// The fused GEMV streams the blocks HBM -> VGPR (one super-block of 256 weights per row
+// per wave-step), dequantises in registers to exactly the bf16 values of the bf16 copy,
+// and feeds v_mfma_f32_16x16x32_bf16 -- decode with Q4_K_M weights therefore computes
+// the same model as prefill, only from 3.6x fewer weight bytes.
+#include "gemv_common.h"
+
+namespace ms {
+
+__device__ __forceinline__ float h2f(uint32_t h16) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)(h16 & 0xFFFFu));
+}
+
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, int i) {  // i compile-time or not
+  const uint32_t w = (i < 4) ? v.x : (i < 8) ? v.y : (i < 12) ? v.z : v.w;
+  return (w >> (8 * (i & 3))) & 0xFFu;
+}
+
+// get_scale_min_k4 on the 12 scale bytes = header bytes 4..15 (v.y, v.z, v.w)
+__device__ __forceinline__ void scale_min_k4(const uint4& hdr, int j, int& d, int& m) {
+  auto q = [&](int i) { return (int)byte_of(hdr, 4 + i); };
+  if (j < 4) {
+    d = q(j) & 63;
+    m = q(j + 4) & 63;
+  } else {
+    d = (q(j + 4) & 0xF) | ((q(j - 4) >> 6) << 4);
+    m = (q(j + 4) >> 4) | ((q(j) >> 6) << 4);
+  }
+}
+
+// ---------------------------------------------------------------- dequantisers
+// one 256-thread block per super-block, thread t -> weight t (the C loop order)
+__device__ __forceinline__ float deq_q4k_one(const uint8_t* b, int t) {
+  const uint4 hdr = *(const uint4*)b;
+  const float d = h2f(hdr.x), dmin = h2f(hdr.x >> 16);
+  const int c = t >> 6, w = t & 63, h = w >> 5, l = w & 31;
+  int sc, m;
+  scale_min_k4(hdr, 2 * c + h, sc, m);
+  const uint32_t qb = b[16 + c * 32 + l];
+  const uint32_t q = h ? (qb >> 4) : (qb & 0xF);
+  const float d1 = __fmul_rn(d, (float)sc), m1 = __fmul_rn(dmin, (float)m);
+  return __fsub_rn(__fmul_rn(d1, (float)q), m1);
+}
+
+// raw ggml Q6_K block: ql[128] qh[64] scales[16] d
+__device__ __forceinline__ float deq_q6k_one(const uint8_t* b, int t) {
+  const int n = t >> 7, r = t & 127, k4 = r >> 5, l = r & 31;
+  const uint32_t a = b[n * 64 + l + ((k4 & 1) ? 32 : 0)];
+  const uint32_t hb = b[128 + n * 32 + l];
+  const int q = (int)(((k4 >> 1) ? (a >> 4) : (a & 0xF)) | (((hb >> (2 * k4)) & 3) << 4)) - 32;
+  const int sc = (int)(int8_t)b[192 + n * 8 + (l >> 4) + 2 * k4];
+  const float d = h2f((uint32_t)b[208] | ((uint32_t)b[209] << 8));
+  return __fmul_rn(__fmul_rn(d, (float)sc), (float)q);
+}
+
+__global__ __launch_bounds__(256) void dequant_f32_kernel(int type, const uint8_t* __restrict__ blocks,
+                                                          float* __restrict__ out) {
+  const size_t sb = blockIdx.x;
+  const int t = threadIdx.x;
+  const float y = (type == MS_QT_Q4_K) ? deq_q4k_one(blocks + sb * kQ4KBytes, t)
+                                       : deq_q6k_one(blocks + sb * kQ6KBytes, t);
+  out[sb * 256 + t] = y;
+}
+
+void launch_dequant_f32(int type, const uint8_t* blocks, int64_t n_blocks, float* out, hipStream_t s) {
+  if (n_blocks <= 0) return;
+  MS_LAUNCH(dequant_f32_kernel, dim3((unsigned)n_blocks), dim3(256), 0, s, type, blocks, out);
+}
+
+// rows of raw blocks -> (a) bf16 rows of the fused matrix, (b) packed quantised rows
+__global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t* __restrict__ blocks,
+                                                         int K, bf16_t* __restrict__ dst_bf16,
+                                                         int map_mul, int map_add,
+                                                         uint8_t* __restrict__ dst_q, int q_row_base) {
+  const int r = blockIdx.y, sb = blockIdx.x, t = threadIdx.x;
+  const int nsb = K / 256;
+  const int braw = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KBytes;
+  const uint8_t* b = blocks + ((size_t)r * nsb + sb) * braw;
+  const float y = (type == MS_QT_Q4_K) ? deq_q4k_one(b, t) : deq_q6k_one(b, t);
+  const size_t drow = map_row(r, map_mul, map_add);
+  dst_bf16[drow * K + (size_t)sb * 256 + t] = f2bf(y);
+  if (dst_q) {
+    const int bp = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KPacked;
+    uint8_t* q = dst_q + ((drow - q_row_base) * nsb + sb) * bp;
+    if (t < braw) q[t] = b[t];  // Q6_K: same field order, d at 208, tail padded below
+    if (type == MS_QT_Q6_K && t >= braw && t < kQ6KPacked) q[t] = 0;
+  }
+}
+
+void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t* dst_bf16, int map_mul,
+                       int map_add, uint8_t* dst_q, int q_row_base, hipStream_t s) {
+  if (rows <= 0) return;
+  MS_LAUNCH(quant_rows_kernel, dim3(K / 256, rows), dim3(256), 0, s, type, blocks, K, dst_bf16,
+            map_mul, map_add, dst_q, q_row_base);
+}
+
+// seeded random blocks (bench / config 5 synthetic weights): every byte from a counter
+// hash, then the fp16 scale fields set so dequantised weights have std ~ `scale`
+__device__ __forceinline__ uint64_t smix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void synth_qblocks_kernel(int type, uint8_t* __restrict__ blocks, int64_t n_blocks,
+                                     uint64_t seed_h, float scale) {
+  const int braw = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KBytes;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_blocks;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t* b = blocks + i * braw;
+    uint64_t h = smix((uint64_t)i ^ seed_h);
+    for (int k = 0; k < braw; k += 8) {
+      h = smix(h);
+      for (int q = 0; q < 8 && k + q < braw; ++q) b[k + q] = (uint8_t)(h >> (8 * q));
+    }
+    const float u = 0.5f + (float)(smix(h) >> 40) * (1.0f / 16777216.0f);
+    if (type == MS_QT_Q4_K) {
+      const _Float16 d = (_Float16)(u * scale / 270.f);
+      const _Float16 dm = (_Float16)((float)d * 7.5f);
+      const uint16_t db = __builtin_bit_cast(uint16_t, d), dmb = __builtin_bit_cast(uint16_t, dm);
+      b[0] = db & 0xFF; b[1] = db >> 8; b[2] = dmb & 0xFF; b[3] = dmb >> 8;
+    } else {
+      for (int k = 0; k < 16; ++k) b[192 + k] = (uint8_t)((int)(b[192 + k] & 0x7F) - 64);
+      const _Float16 d = (_Float16)(u * scale / 680.f);
+      const uint16_t db = __builtin_bit_cast(uint16_t, d);
+      b[208] = db & 0xFF; b[209] = db >> 8;
+    }
+  }
+}
+
+void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t seed, float scale,
+                          hipStream_t s) {
+  MS_LAUNCH(synth_qblocks_kernel, dim3(2048), dim3(256), 0, s, type, blocks, n_blocks,
+            (uint64_t)smix_host(seed), scale);
+}
+
+// ---------------------------------------------------------------- dequant-fused GEMV
+// One block per 16*NT rows, waves split the K/256 super-blocks (SBW per wave).  Lane
+// group g = lane>>4 owns 64 weights of each super-block:
+//   Q4_K: chunk g (qs bytes 32g..32g+31): low nibbles = weights 64g..64g+31 (sub-block
+//         2g), high nibbles = 64g+32.. (sub-block 2g+1);
+//   Q6_K: half h = g>>1, positions l in [16p, 16p+16), p = g&1, each giving the four
+//         weights h*128 + {0,32,64,96} + l.
+// MFMA t of a super-block takes 8 of those weights per lane and the X elements of the
+// same k -- a k permutation applied to both operands, so every dot product is unchanged.
+template <int MT, int NT, int EPI, int SBW>
+__global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
+                                                     void* __restrict__ out, int M, int N, int K,
+                                                     int ldo, GemvArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16 * NT;
+  // the region holding this tile (regions are 16-row aligned; block-uniform)
+  int type = qm.type0, row_bytes = qm.row_bytes0, rbase = n0 - qm.row0_0;
+  const uint8_t* base = qm.base0;
+  if (qm.n > 1 && n0 >= qm.row0_1) { type = qm.type1; row_bytes = qm.row_bytes1; rbase = n0 - qm.row0_1; base = qm.base1; }
+  if (qm.n > 2 && n0 >= qm.row0_2) { type = qm.type2; row_bytes = qm.row_bytes2; rbase = n0 - qm.row0_2; base = qm.base2; }
+  const int sb0 = wave * SBW;
+  const size_t xstride = 2 * (size_t)K + 16;
+
+  f32x4 acc[MT][NT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (type == MS_QT_Q4_K) {
+    uint4 hq[SBW][NT], q0[SBW][NT], q1[SBW][NT];
+#pragma unroll
+    for (int j = 0; j < SBW; ++j)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sb0 + j) * kQ4KBytes;
+        hq[j][n] = ldg16(bp);
+        q0[j][n] = ldg16(bp + 16 + 32 * g);
+        q1[j][n] = ldg16(bp + 32 + 32 * g);
+      }
+    gemv_stage_x(smem, X, M, K);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SBW; ++j)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const float d = h2f(hq[j][n].x), dmin = h2f(hq[j][n].x >> 16);
+        int s0, m0, s1, m1;
+        scale_min_k4(hq[j][n], 2 * g, s0, m0);
+        scale_min_k4(hq[j][n], 2 * g + 1, s1, m1);
+        const float dl[2] = {__fmul_rn(d, (float)s0), __fmul_rn(d, (float)s1)};
+        const float ml[2] = {__fmul_rn(dmin, (float)m0), __fmul_rn(dmin, (float)m1)};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int h = t >> 2, c = t & 3;
+          const uint4& qq = (c < 2) ? q0[j][n] : q1[j][n];
+          const uint32_t w0 = (c & 1) ? qq.z : qq.x, w1 = (c & 1) ? qq.w : qq.y;
+          uint32_t pk[4];
+#pragma unroll
+          for (int i = 0; i < 8; i += 2) {
+            const uint32_t wd = (i < 4) ? w0 : w1;
+            const uint32_t b0 = (wd >> (8 * (i & 3))) & 0xFF, b1 = (wd >> (8 * ((i + 1) & 3))) & 0xFF;
+            const uint32_t n0q = h ? (b0 >> 4) : (b0 & 0xF), n1q = h ? (b1 >> 4) : (b1 & 0xF);
+            const float y0 = __fsub_rn(__fmul_rn(dl[h], (float)n0q), ml[h]);
+            const float y1 = __fsub_rn(__fmul_rn(dl[h], (float)n1q), ml[h]);
+            pk[i >> 1] = pack2bf(y0, y1);
+          }
+          const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
+          const int k = (sb0 + j) * 256 + g * 64 + h * 32 + c * 8;
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int xrow = min(m * 16 + fr, M - 1);
+            const bf16x8 xf = *(const bf16x8*)(smem + xrow * xstride + k * 2);
+            acc[m][n] = mfma16(xf, wf, acc[m][n]);
+          }
+        }
+      }
+  } else {  // Q6_K, packed 224-B blocks
+    const int hh = g >> 1, p = g & 1;
+    uint4 qa[SBW][NT], qb[SBW][NT], qh[SBW][NT], sc[SBW][NT];
+    uint32_t dw[SBW][NT];
+#pragma unroll
+    for (int j = 0; j < SBW; ++j)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sb0 + j) * kQ6KPacked;
+        qa[j][n] = ldg16(bp + hh * 64 + 16 * p);
+        qb[j][n] = ldg16(bp + hh * 64 + 32 + 16 * p);
+        qh[j][n] = ldg16(bp + 128 + hh * 32 + 16 * p);
+        sc[j][n] = ldg16(bp + 192);
+        dw[j][n] = *(const uint32_t*)(bp + 208);
+      }
+    gemv_stage_x(smem, X, M, K);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SBW; ++j)
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const float d = h2f(dw[j][n]);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int k4 = t >> 1, sub = t & 1;
+          const int si = hh * 8 + p + 2 * k4;
+          const float ds = __fmul_rn(d, (float)(int)(int8_t)byte_of(sc[j][n], si));
+          uint32_t pk[4];
+#pragma unroll
+          for (int i = 0; i < 8; i += 2) {
+            float y[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int li = 8 * sub + i + e;
+              const uint32_t a = byte_of((k4 & 1) ? qb[j][n] : qa[j][n], li);
+              const uint32_t hb = byte_of(qh[j][n], li);
+              const int q = (int)(((k4 >> 1) ? (a >> 4) : (a & 0xF)) | (((hb >> (2 * k4)) & 3) << 4)) - 32;
+              y[e] = __fmul_rn(ds, (float)q);
+            }
+            pk[i >> 1] = pack2bf(y[0], y[1]);
+          }
+          const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
+          const int k = (sb0 + j) * 256 + hh * 128 + k4 * 32 + 16 * p + 8 * sub;
+#pragma unroll
+          for (int m = 0; m < MT; ++m) {
+            const int xrow = min(m * 16 + fr, M - 1);
+            const bf16x8 xf = *(const bf16x8*)(smem + xrow * xstride + k * 2);
+            acc[m][n] = mfma16(xf, wf, acc[m][n]);
+          }
+        }
+      }
+  }
+  gemv_finish<MT, NT, EPI>(acc, smem, M, N, ldo, out, n0, ga);
+}
+
+struct QPlan {
+  int MT, NT, SBW, waves, tiles;
+};
+
+static QPlan qplan(int M, int N, int K, int epi) {
+  QPlan p{};
+  p.MT = (M + 15) / 16;
+  p.NT = (epi == MS_GEMV_EPI_SWIGLU) ? 2 : 1;
+  p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
+  const int nsb = K / 256;
+  p.SBW = nsb > 16 ? 2 : 1;
+  p.waves = (nsb % p.SBW == 0) ? nsb / p.SBW : 0;
+  if (p.waves > 16) p.waves = 0;
+  return p;
+}
+
+static size_t qlds(const QPlan& p, int M, int K) {
+  const size_t xs = (size_t)M * (2 * (size_t)K + 16);
+  const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
+  return xs > red ? xs : red;
+}
+
+bool qgemv_supported(int M, int N, int K, int epi) {
+  if (M < 1 || M > 64 || K % 256 || N % 16) return false;
+  if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
+  const QPlan p = qplan(M, N, K, epi);
+  return p.waves > 0 && qlds(p, M, K) <= 160 * 1024;
+}
+
+template <int MT, int NT, int EPI>
+static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
+                     const QPlan& p, const GemvArgs& ga, hipStream_t s) {
+  const size_t lds = qlds(p, M, K);
+  const dim3 grid(p.tiles), blk(64 * p.waves);
+  if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
+    return;
+  } else {
+    if (p.SBW == 2)
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 2>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+    else
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 1>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+  }
+}
+
+template <int MT>
+static void qgemv_go_mt(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+                        const QPlan& p, const GemvArgs& ga, hipStream_t s) {
+  switch (epi) {
+    case MS_GEMV_EPI_STORE_BF16: qgemv_go<MT, 1, MS_GEMV_EPI_STORE_BF16>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    case MS_GEMV_EPI_ADD_F32: qgemv_go<MT, 1, MS_GEMV_EPI_ADD_F32>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    case MS_GEMV_EPI_SWIGLU: qgemv_go<MT, 2, MS_GEMV_EPI_SWIGLU>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    case MS_GEMV_EPI_ROPE_KV: qgemv_go<MT, 1, MS_GEMV_EPI_ROPE_KV>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    default: qgemv_go<MT, 1, MS_GEMV_EPI_STORE_F32>(X, q, out, M, N, K, ldo, p, ga, s); break;
+  }
+}
+
+void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+                  const GemvArgs* ga_in, hipStream_t s) {
+  if (M <= 0) return;
+  const QPlan p = qplan(M, N, K, epi);
+  if (p.waves == 0) return;  // callers check qgemv_supported()
+  GemvArgs ga{};
+  if (ga_in) ga = *ga_in;
+  switch (p.MT) {
+    case 1: qgemv_go_mt<1>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
+    case 2: qgemv_go_mt<2>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
+    case 3: qgemv_go_mt<3>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
+    default: qgemv_go_mt<4>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
+  }
+}
+
+}  // namespace ms

@@ -69,6 +69,37 @@ void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int 
 void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, const GemvArgs* ga, int force_waves, hipStream_t s);
 
+// ---- ggml K-quant weights (k_qgemv.hip)
+enum { MS_QT_Q4_K = 12, MS_QT_Q6_K = 14 };  // ggml_type ids
+constexpr int kQ4KBytes = 144, kQ6KBytes = 210, kQ6KPacked = 224;
+// up to 3 row regions of one fused matrix, each of a single K-quant type (flat fields:
+// no runtime-indexed kernel-argument arrays)
+struct QMat {
+  int n;
+  const uint8_t* base0; int row0_0, type0, row_bytes0;
+  const uint8_t* base1; int row0_1, type1, row_bytes1;
+  const uint8_t* base2; int row0_2, type2, row_bytes2;
+};
+inline uint64_t smix_host(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+inline int qblock_bytes(int type, bool packed) {
+  return type == MS_QT_Q4_K ? kQ4KBytes : (packed ? kQ6KPacked : kQ6KBytes);
+}
+void launch_dequant_f32(int type, const uint8_t* blocks, int64_t n_blocks, float* out, hipStream_t s);
+// raw ggml rows [rows][K/256 blocks] -> bf16 rows of a fused matrix (map_row) and, if dst_q,
+// packed quantised rows at (map_row(r) - q_row_base)
+void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t* dst_bf16,
+                       int map_mul, int map_add, uint8_t* dst_q, int q_row_base, hipStream_t s);
+void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t seed, float scale,
+                          hipStream_t s);
+bool qgemv_supported(int M, int N, int K, int epi);
+void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+                  const GemvArgs* ga, hipStream_t s);
+
 void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s);
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len);

@@ -19,11 +19,13 @@ MS_FLAG_IGNORE_EOS = 1
 (MS_T_EMBED, MS_T_ATTN_NORM, MS_T_WQ, MS_T_WK, MS_T_WV, MS_T_WO, MS_T_FFN_NORM, MS_T_WGATE,
  MS_T_WUP, MS_T_WDOWN, MS_T_FINAL_NORM, MS_T_LM_HEAD) = range(12)
 MS_EPI_STORE_BF16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
+MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms
 K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC = range(6)
 
 EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
+    "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv",
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_rmsnorm", "ms_op_argmax",
@@ -75,6 +77,11 @@ def load() -> C.CDLL:
         "ms_last_error": (C.c_char_p, [vp]),
         "ms_load_weight": (i32, [vp, i32, i32, vp, i64]),
         "ms_init_synthetic": (i32, [vp, u64, C.c_float, C.c_float]),
+        "ms_load_weight_q": (i32, [vp, i32, i32, i32, vp, i64]),
+        "ms_init_synthetic_q": (i32, [vp, u64, C.c_float, C.c_float]),
+        "ms_op_dequant": (i32, [i32, vp, i64, vp, vp]),
+        "ms_op_quant_rows": (i32, [i32, vp, i32, i32, vp, vp, vp]),
+        "ms_op_qgemv": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_submit": (i32, [vp, pi32, i32, i32, u32, u64]),
         "ms_step": (i32, [vp]),
         "ms_poll": (i32, [vp, C.POINTER(MsResult), i32]),

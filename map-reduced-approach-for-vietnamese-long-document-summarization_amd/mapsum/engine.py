@@ -81,6 +81,15 @@ class Engine:
     def init_synthetic(self, seed: int = 0, std: float = 0.02, norm_jitter: float = 0.0):
         self._chk(self.lib.ms_init_synthetic(self.h, seed, std, norm_jitter), "ms_init_synthetic")
 
+    def init_synthetic_q(self, seed: int = 2, scale: float = 0.02, norm_jitter: float = 0.0):
+        """Random Q4_K/Q6_K blocks in the Q4_K_M per-tensor mix (BASELINE config 5)."""
+        self._chk(self.lib.ms_init_synthetic_q(self.h, seed, scale, norm_jitter), "ms_init_synthetic_q")
+
+    def load_tensor_q(self, tensor: int, layer: int, ggml_type: int, blocks: np.ndarray):
+        b = np.ascontiguousarray(blocks, dtype=np.uint8)
+        self._chk(self.lib.ms_load_weight_q(self.h, tensor, layer, ggml_type, b.ctypes.data, b.size),
+                  "ms_load_weight_q")
+
     def load_tensor(self, tensor: int, layer: int, bf16_bits: np.ndarray):
         a = np.ascontiguousarray(bf16_bits, dtype=np.uint16)
         self._chk(self.lib.ms_load_weight(self.h, tensor, layer, a.ctypes.data, a.size), "ms_load_weight")

@@ -46,6 +46,27 @@ def load_logical(engine, w: dict):
         up(L.MS_T_WDOWN, i, ly["w_down"])
 
 
+_Q_NAMES = {"embed": L.MS_T_EMBED, "lm_head": L.MS_T_LM_HEAD, "wq": L.MS_T_WQ, "wk": L.MS_T_WK,
+            "wv": L.MS_T_WV, "wo": L.MS_T_WO, "w_gate": L.MS_T_WGATE, "w_up": L.MS_T_WUP,
+            "w_down": L.MS_T_WDOWN}
+
+
+def load_quantized(engine, qw: dict, norms: dict):
+    """Upload a K-quant model: qw[name] = (ggml_type, uint8 blocks) for "embed"/"lm_head" and
+    qw[(layer, name)] for the per-layer matrices (rows of raw ggml blocks, GGUF order after
+    Q/K un-permutation); norms = {"final_norm": f32, "layers": [{"attn_norm", "ffn_norm"}]}."""
+    cfg = engine.cfg
+    for key, (qt, blocks) in qw.items():
+        layer, name = (0, key) if isinstance(key, str) else key
+        engine.load_tensor_q(_Q_NAMES[name], layer, qt, blocks)
+    engine.load_tensor(L.MS_T_FINAL_NORM, 0, f32_to_bf16_bits(norms["final_norm"]))
+    for i, ly in enumerate(norms["layers"]):
+        engine.load_tensor(L.MS_T_ATTN_NORM, i, f32_to_bf16_bits(ly["attn_norm"]))
+        engine.load_tensor(L.MS_T_FFN_NORM, i, f32_to_bf16_bits(ly["ffn_norm"]))
+    if len([k for k in qw if not isinstance(k, str)]) != 7 * cfg.n_layers:
+        raise RuntimeError("quantised model is missing per-layer matrices")
+
+
 _HF_LAYER = {
     "input_layernorm.weight": L.MS_T_ATTN_NORM,
     "self_attn.q_proj.weight": L.MS_T_WQ,

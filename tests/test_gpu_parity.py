@@ -286,3 +286,125 @@ def test_unfused_decode_path_large_batch(oracle):
         assert matched / (20 * 8) >= 0.97, matched
     finally:
         e.close()
+
+
+# ------------------------------------------------------------------ K-quant (config 5)
+from oracle import quants as Q  # noqa: E402
+
+
+@pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
+def test_dequant_bit_exact_vs_c_oracle(lib, dev, qtype):
+    b = Q.random_blocks(qtype, 777, seed=5)
+    if qtype == Q.GGML_TYPE_Q4_K:
+        b[0, 0:2] = [0x01, 0x00]; b[1, 2:4] = [0x00, 0x80]; b[2, 4:16] = 0xFF; b[3, 16:] = 0xFF
+        b[4, 0:2] = [0xFF, 0x7B]  # d = 65504 (largest finite fp16)
+    else:
+        b[0, 208:210] = [0x01, 0x00]; b[1, 192:208] = 0x80; b[2, 0:192] = 0xFF
+    want = Q.c_dequant(b, qtype)
+    bd = torch.from_numpy(b.reshape(-1)).to(dev)
+    out = torch.empty(want.size, dtype=torch.float32, device=dev)
+    L.check(lib.ms_op_dequant(qtype, bd.data_ptr(), b.shape[0], out.data_ptr(), _stream()))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), "dequant must be bit-exact"
+
+
+def _packed(lib, dev, qtype, rows, K, seed):
+    b = Q.random_blocks(qtype, rows * K // 256, seed=seed)
+    bd = torch.from_numpy(b.reshape(-1)).to(dev)
+    wbf = torch.empty(rows, K, dtype=torch.bfloat16, device=dev)
+    pk = torch.empty(rows * (K // 256) * (144 if qtype == Q.GGML_TYPE_Q4_K else 224), dtype=torch.uint8, device=dev)
+    L.check(lib.ms_op_quant_rows(qtype, bd.data_ptr(), rows, K, wbf.data_ptr(), pk.data_ptr(), _stream()))
+    torch.cuda.synchronize()
+    return b, wbf, pk
+
+
+@pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
+def test_quant_rows_bf16_copy_is_rounded_dequant(lib, dev, qtype):
+    b, wbf, _ = _packed(lib, dev, qtype, 48, 768, 6)
+    want = Q.c_dequant(b, qtype).reshape(48, 768)
+    from oracle.synth import bf16_rne
+    got = wbf.float().cpu().numpy()
+    assert np.array_equal(got, bf16_rne(want))
+
+
+@pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
+@pytest.mark.parametrize("M", [1, 8, 16, 33])
+@pytest.mark.parametrize("N,K,epi", [(256, 768, L.MS_EPI_STORE_BF16), (512, 2048, L.MS_EPI_ADD_F32),
+                                     (1024, 768, L.MS_EPI_SWIGLU), (128, 8192, L.MS_EPI_STORE_F32)])
+def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
+    _, wbf, pk = _packed(lib, dev, qtype, N, K, 7 + M)
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ref = X.float() @ wbf.float().T
+    if epi == L.MS_EPI_SWIGLU:
+        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        r = ref.view(M, N // 32, 2, 16)
+        exp = (torch.nn.functional.silu(r[:, :, 0, :]) * r[:, :, 1, :]).reshape(M, N // 2)
+        ldo = N // 2
+    elif epi == L.MS_EPI_STORE_BF16:
+        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        exp, ldo = ref, N
+    elif epi == L.MS_EPI_ADD_F32:
+        out = torch.randn(M, N, generator=g).to(dev)
+        exp, ldo = out.clone() + ref, N
+    else:
+        out = torch.zeros(M, N, dtype=torch.float32, device=dev)
+        exp, ldo = ref, N
+    L.check(lib.ms_op_qgemv(X.data_ptr(), qtype, pk.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, _stream()))
+    torch.cuda.synchronize()
+    assert rel(out.float().cpu(), exp.cpu()) < 1e-2
+
+
+def _quant_model(seed):
+    """Tiny Q4_K_M-style model: raw blocks per matrix + the oracle's view of it
+    (weights = bf16_rne(dequant(blocks)))."""
+    from oracle.synth import bf16_rne, make_weights
+    base = make_weights(TINY, SEED, std=STD, jitter=JITTER)  # norms reused
+    H, D, F, V = TINY.hidden, TINY.head_dim, TINY.ffn, TINY.vocab
+    shapes = {"wq": (TINY.n_heads * D, H), "wk": (TINY.n_kv_heads * D, H), "wv": (TINY.n_kv_heads * D, H),
+              "wo": (H, TINY.n_heads * D), "w_gate": (F, H), "w_up": (F, H), "w_down": (H, F)}
+    qw, w = {}, {"final_norm": base["final_norm"], "layers": []}
+    qt = Q.q4_k_m_type("embed", 0, TINY.n_layers)
+    eb = Q.random_blocks(qt, V * H // 256, seed=seed, scale=STD)
+    qw["embed"] = (qt, eb)
+    w["embed"] = bf16_rne(Q.dequant(eb, qt)).reshape(V, H)
+    w["lm_head"] = w["embed"]
+    for l in range(TINY.n_layers):
+        ly = {"attn_norm": base["layers"][l]["attn_norm"], "ffn_norm": base["layers"][l]["ffn_norm"]}
+        for i, (name, (r, c)) in enumerate(shapes.items()):
+            qt = Q.q4_k_m_type(name, l, TINY.n_layers)
+            blk = Q.random_blocks(qt, r * c // 256, seed=seed * 1000 + l * 10 + i, scale=STD)
+            qw[(l, name)] = (qt, blk)
+            ly[name] = bf16_rne(Q.dequant(blk, qt)).reshape(r, c)
+        w["layers"].append(ly)
+    return qw, w
+
+
+def test_quantized_engine_greedy_vs_oracle(dev):
+    """Config 5 end to end on the tiny model: K-quant decode GEMVs (fused path, B <= 16)
+    and bf16(dequant) prefill against the oracle run on the same dequantised weights."""
+    from mapsum.weights import load_quantized
+    qw, w = _quant_model(3)
+    # the 2-layer tiny model uses the Q4_K_M mix: both types occur
+    kinds = {qt for (qt, _) in qw.values()}
+    assert kinds == {Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K}
+    oracle_q = OracleLlama(TINY, w)
+    e = Engine(TINY, device=0, max_batch=4, max_ctx=512, max_prefill_tokens=2048)
+    try:
+        load_quantized(e, qw, w)
+        prompts = [_prompt(n, 700 + n) for n in (17, 140, 301)]
+        res = e.generate(prompts, num_predict=24, ignore_eos=True)
+        matched = 0
+        for p, r in zip(prompts, res):
+            ref, _ = oracle_q.generate(p, 24, ignore_eos=True)
+            k = 0
+            while k < 24 and r.ids[k] == ref[k]:
+                k += 1
+            matched += k
+        assert matched / (3 * 24) >= 0.99, matched
+        _, lg = e.forward(prompts[1], hidden=False, logits=True)
+        ref_lg, _ = oracle_q.forward(prompts[1], all_logits=True)
+        assert rel(lg, ref_lg) < 2e-2
+    finally:
+        e.close()
