@@ -159,7 +159,7 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 //         weights h*128 + {0,32,64,96} + l.
 // MFMA t of a super-block takes 8 of those weights per lane and the X elements of the
 // same k -- a k permutation applied to both operands, so every dot product is unchanged.
-template <int MT, int NT, int EPI, int SBW>
+template <int MT, int NT, int EPI, int SBW, bool XL>
 __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, GemvArgs ga) {
@@ -192,8 +192,10 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         q0[j][n] = ldg16(bp + 16 + 32 * g);
         q1[j][n] = ldg16(bp + 32 + 32 * g);
       }
-    gemv_stage_x(smem, X, M, K);
-    __syncthreads();
+    if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
+      gemv_stage_x(smem, X, M, K);
+      __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
@@ -224,7 +226,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = *(const bf16x8*)(smem + xrow * xstride + k * 2);
+            const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
+                                 : *(const bf16x8*)(X + (size_t)xrow * K + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
         }
@@ -244,8 +247,10 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         sc[j][n] = ldg16(bp + 192);
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
-    gemv_stage_x(smem, X, M, K);
-    __syncthreads();
+    if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
+      gemv_stage_x(smem, X, M, K);
+      __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
@@ -275,7 +280,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = *(const bf16x8*)(smem + xrow * xstride + k * 2);
+            const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
+                                 : *(const bf16x8*)(X + (size_t)xrow * K + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
         }
@@ -300,8 +306,12 @@ static QPlan qplan(int M, int N, int K, int epi) {
   return p;
 }
 
+static constexpr size_t kLdsCap = 160 * 1024;
+
+static bool qx_in_lds(int M, int K) { return (size_t)M * (2 * (size_t)K + 16) <= kLdsCap; }
+
 static size_t qlds(const QPlan& p, int M, int K) {
-  const size_t xs = (size_t)M * (2 * (size_t)K + 16);
+  const size_t xs = qx_in_lds(M, K) ? (size_t)M * (2 * (size_t)K + 16) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
@@ -310,7 +320,7 @@ bool qgemv_supported(int M, int N, int K, int epi) {
   if (M < 1 || M > 64 || K % 256 || N % 16) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
   const QPlan p = qplan(M, N, K, epi);
-  return p.waves > 0 && qlds(p, M, K) <= 160 * 1024;
+  return p.waves > 0 && qlds(p, M, K) <= kLdsCap;
 }
 
 template <int MT, int NT, int EPI>
@@ -321,10 +331,15 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;
   } else {
-    if (p.SBW == 2)
-      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 2>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+    const bool xl = qx_in_lds(M, K);
+    if (p.SBW == 2 && xl)
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 2, true>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+    else if (p.SBW == 2)
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 2, false>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+    else if (xl)
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 1, true>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
     else
-      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 1>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, 1, false>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga);
   }
 }
 

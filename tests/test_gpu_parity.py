@@ -336,7 +336,10 @@ def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
     _, wbf, pk = _packed(lib, dev, qtype, N, K, 7 + M)
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
-    ref = X.float() @ wbf.float().T
+    # fp64 reference on the host: fp32 outputs may differ only by summation order, bf16
+    # outputs additionally by one rounding
+    ref = (X.double().cpu() @ wbf.double().cpu().T).to(dev)
+    tol = 2e-6 if epi in (L.MS_EPI_STORE_F32, L.MS_EPI_ADD_F32) else 4e-3
     if epi == L.MS_EPI_SWIGLU:
         out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
         r = ref.view(M, N // 32, 2, 16)
@@ -347,13 +350,13 @@ def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
         exp, ldo = ref, N
     elif epi == L.MS_EPI_ADD_F32:
         out = torch.randn(M, N, generator=g).to(dev)
-        exp, ldo = out.clone() + ref, N
+        exp, ldo = out.double() + ref, N
     else:
         out = torch.zeros(M, N, dtype=torch.float32, device=dev)
         exp, ldo = ref, N
     L.check(lib.ms_op_qgemv(X.data_ptr(), qtype, pk.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, _stream()))
     torch.cuda.synchronize()
-    assert rel(out.float().cpu(), exp.cpu()) < 1e-2
+    assert rel(out.double().cpu(), exp.cpu()) < tol
 
 
 def _quant_model(seed):
@@ -381,6 +384,21 @@ def _quant_model(seed):
     return qw, w
 
 
+def _teacher_forced_agreement(oracle, prompt, gen):
+    """Per-step greedy agreement: the oracle is run over prompt + the engine's own tokens
+    (teacher forcing, so one near-tie flip does not cascade) and its argmax at each step
+    is compared with the engine's token.  Returns (agreeing steps, [(step, oracle top-2
+    gap, oracle top logit)] at the steps that differ)."""
+    ids = np.concatenate([np.asarray(prompt, np.int32), np.asarray(gen[:-1], np.int32)])
+    lg, _ = oracle.forward(ids, all_logits=True)
+    lg = lg[len(prompt) - 1:]
+    want = np.argmax(lg, 1)
+    srt = np.sort(lg, 1)
+    flips = [(i, float(srt[i, -1] - lg[i, gen[i]]), float(srt[i, -1]))
+             for i in range(len(gen)) if want[i] != gen[i]]
+    return len(gen) - len(flips), flips
+
+
 def test_quantized_engine_greedy_vs_oracle(dev):
     """Config 5 end to end on the tiny model: K-quant decode GEMVs (fused path, B <= 16)
     and bf16(dequant) prefill against the oracle run on the same dequantised weights."""
@@ -393,16 +411,20 @@ def test_quantized_engine_greedy_vs_oracle(dev):
     e = Engine(TINY, device=0, max_batch=4, max_ctx=512, max_prefill_tokens=2048)
     try:
         load_quantized(e, qw, w)
-        prompts = [_prompt(n, 700 + n) for n in (17, 140, 301)]
-        res = e.generate(prompts, num_predict=24, ignore_eos=True)
-        matched = 0
+        prompts = [_prompt(n, 700 + n) for n in (17, 140, 301, 64)]
+        res = e.generate(prompts, num_predict=48, ignore_eos=True)
+        agree = total = 0
         for p, r in zip(prompts, res):
-            ref, _ = oracle_q.generate(p, 24, ignore_eos=True)
-            k = 0
-            while k < 24 and r.ids[k] == ref[k]:
-                k += 1
-            matched += k
-        assert matched / (3 * 24) >= 0.99, matched
+            a, flips = _teacher_forced_agreement(oracle_q, p, r.ids)
+            agree += a
+            total += len(r.ids)
+            # a decode token the oracle would not pick is only acceptable at a near-tie
+            # of the oracle's own logits (K-quant decode sums in another fp32 order)
+            for pos, gap, top in flips:
+                assert gap <= 1e-2 * (abs(top) + 1.0), (pos, gap, top)
+        # the random tiny model has flat logits (12 % of positions have an oracle top-2
+        # gap < 0.05), so near-tie flips are common; the bar is the all-position test's
+        assert agree / total >= 0.97, (agree, total)
         _, lg = e.forward(prompts[1], hidden=False, logits=True)
         ref_lg, _ = oracle_q.forward(prompts[1], all_logits=True)
         assert rel(lg, ref_lg) < 2e-2

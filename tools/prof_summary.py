@@ -1,11 +1,25 @@
-"""Summarise a rocprofv3 --stats kernel_stats.csv: per-kernel calls / total / average."""
+"""Summarise a rocprofv3 kernel trace: per-kernel calls / total / average.
+
+Accepts either the --stats kernel_stats.csv (``--output-format csv``) or the default
+rocpd SQLite database (``*_results.db``, view ``top_kernels``)."""
 import csv
+import sqlite3
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
-tot = sum(float(r["TotalDurationNs"]) for r in rows)
+
+def rows_of(path):
+    if path.endswith(".db"):
+        c = sqlite3.connect(path)
+        for name, calls, total, avg, _ in c.execute("select * from top_kernels"):
+            yield name, int(calls), float(total), float(avg)  # ns
+    else:
+        for r in csv.DictReader(open(path)):
+            yield r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"])
+
+
+rows = sorted(rows_of(sys.argv[1]), key=lambda r: -r[2])
+tot = sum(r[2] for r in rows)
 print(f"{'kernel':78s} {'calls':>7s} {'total_ms':>10s} {'avg_us':>9s} {'pct':>6s}")
-for r in rows:
-    print(f"{r['Name'][:78]:78s} {int(r['Calls']):7d} {float(r['TotalDurationNs'])/1e6:10.2f} "
-          f"{float(r['AverageNs'])/1e3:9.2f} {100*float(r['TotalDurationNs'])/tot:6.1f}")
-print(f"{'TOTAL':78s} {'':7s} {tot/1e6:10.2f}")
+for name, calls, total, avg in rows:
+    print(f"{name[:78]:78s} {calls:7d} {total / 1e6:10.2f} {avg / 1e3:9.2f} {100 * total / tot:6.1f}")
+print(f"{'TOTAL':78s} {'':7s} {tot / 1e6:10.2f}")
