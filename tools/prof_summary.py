@@ -11,7 +11,7 @@ def rows_of(path):
     if path.endswith(".db"):
         c = sqlite3.connect(path)
         for name, calls, total, avg, _ in c.execute("select * from top_kernels"):
-            yield name, int(calls), float(total), float(avg)  # ns
+            yield name, int(calls), float(total) * 1e3, float(avg) * 1e3  # view is in us
     else:
         for r in csv.DictReader(open(path)):
             yield r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"])
