@@ -171,6 +171,13 @@ int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, in
 /* tuning hook: as ms_op_gemv with the K-splitting wave count forced (0 = heuristic) */
 int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                      int32_t ldo, int32_t epilogue, void* workspace, int32_t waves, void* stream);
+/* decode split-K: slabs fp32 [S][M][N], slab s = X[:, sK/S:(s+1)K/S] . W[:, same]^T;
+   waves = 0 picks the heuristic (tuning hook otherwise) */
+int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
+                     int32_t S, int32_t waves, void* stream);
+/* x fp32 [rows][hidden] += slab_0 + ... + slab_{S-1} (slab order); y bf16 = rmsnorm(x) * w */
+int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y,
+                           int32_t rows, int32_t hidden, float eps, void* stream);
 /* K-quant ops: raw ggml blocks -> fp32 (bit-exact restatement of llama.cpp's
    dequantize_row_q4_K/q6_K); raw rows -> bf16 rows + packed rows (Q6_K repacked to 224 B);
    dequant-fused GEMV over packed rows (same epilogues as ms_op_gemv) */

@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <array>
@@ -106,6 +107,13 @@ struct ms_engine {
   int32_t* ids_out_d = nullptr;
   void* gemv_ws = nullptr;
   float* attn_ws = nullptr;
+  // decode O / down projections: split-K partial slabs [S][B][H] fp32, folded into the
+  // residual by the next residual_rmsnorm launch (pending_split = S of the unfolded slabs)
+  float* slabs = nullptr;
+  int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
+  // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
+  // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
+  bool attn_slabs = true, attn_fused_combine = false;
   int32_t* args_d = nullptr;
   int32_t* args_h = nullptr;  // pinned
   size_t args_cap = 0;
@@ -200,41 +208,69 @@ struct ms_engine {
     prof_end(cls);
   }
 
-  // decode with fused epilogues: norm, QKV+RoPE+KV-scatter, attention(+combine), O(+res),
-  // norm, gate/up+SwiGLU, down(+res) -- 8 launches per layer instead of 9
+  // decode with fused epilogues: residual+norm, QKV+RoPE+KV-scatter, attention(+combine),
+  // O (split-K slabs), residual+norm, gate/up+SwiGLU, down (split-K slabs)
   bool fused_decode(int B) const {
-    return gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV) &&
-           gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
-           gemv_supported(B, H, Hq * D, MS_GEMV_EPI_ADD_F32) &&
-           gemv_supported(B, H, F, MS_GEMV_EPI_ADD_F32);
+    return B <= kMaxSlabRows && residual_rmsnorm_supported(kMaxSplit, H) &&
+           (attn_slabs ? gemv_split_supported(B, QKVN, H, 1) : gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
+           gemv_split_supported(B, H, Hq * D, 1) && gemv_split_supported(B, H, F, 1) &&
+           attn_decode_supported(B, Hq, Hk, max_pages * kPage);
+  }
+  static constexpr int kMaxSlabRows = 64, kMaxSplit = 8;
+
+  // projection into fp32 partial slabs [S][M][N]; returns the number of slabs written
+  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S) {
+    prof_begin(K_GEMV);
+    int used = 1;
+    if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
+      launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
+    } else {
+      if (!(S >= 1 && S <= kMaxSplit && gemv_split_supported(M, N, K, S))) S = 1;
+      launch_gemv_split(X, W, slabs, M, N, K, S, 0, stream);
+      used = S;
+    }
+    prof_end(K_GEMV);
+    return used;
+  }
+
+  // fold pending slabs into x, then RMSNorm(x) * w -> xb
+  void residual_norm(const bf16_t* w, int B) {
+    prof_begin(K_MISC);
+    launch_residual_rmsnorm(x, slabs, pending_split, w, xb, B, H, cfg.norm_eps, stream);
+    prof_end(K_MISC);
+    pending_split = 0;
   }
 
   void run_layer_fused_decode(int l, int B, const int32_t* tok_pos, const int32_t* tok_slot,
                               const DecodeAttnArgs& da) {
     const Layer& Ly = layers[l];
     KVView kv = kv_layer(l);
-    prof_begin(K_MISC);
-    launch_rmsnorm(x, Ly.attn_norm, xb, B, H, cfg.norm_eps, nullptr, stream);
-    prof_end(K_MISC);
-    GemvArgs ga{};
-    ga.tok_pos = tok_pos;
-    ga.tok_slot = tok_slot;
-    ga.cos_tab = cos_tab;
-    ga.sin_tab = sin_tab;
-    ga.kv = kv;
-    ga.Hq = Hq;
-    ga.Hk = Hk;
+    residual_norm(Ly.attn_norm, B);
     const auto& Q = lq[l];
-    proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
+    DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab};
+    if (attn_slabs) {
+      // QKV -> slabs; attention adds them, applies RoPE and writes the new K/V (k_attn.hip)
+      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv);
+    } else {
+      // QKV GEMV epilogue: RoPE, q -> qkv rows, K/V -> paged cache
+      GemvArgs ga{};
+      ga.tok_pos = tok_pos;
+      ga.tok_slot = tok_slot;
+      ga.cos_tab = cos_tab;
+      ga.sin_tab = sin_tab;
+      ga.kv = kv;
+      ga.Hq = Hq;
+      ga.Hk = Hk;
+      proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
+      qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab};
+    }
     prof_begin(K_ATTN_DECODE);
-    launch_attn_decode(qkv, attn, Hq, Hk, kv, da, attn_ws, stream);
+    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
     prof_end(K_ATTN_DECODE);
-    proj(&Q[QS_O], attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_ADD_F32, nullptr, K_GEMV);
-    prof_begin(K_MISC);
-    launch_rmsnorm(x, Ly.ffn_norm, xb, B, H, cfg.norm_eps, nullptr, stream);
-    prof_end(K_MISC);
+    pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o);
+    residual_norm(Ly.ffn_norm, B);
     proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
-    proj(&Q[QS_DOWN], hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_ADD_F32, nullptr, K_GEMV);
+    pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down);
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
@@ -256,7 +292,7 @@ struct ms_engine {
     prof_end(K_MISC);
     if (decode) {
       prof_begin(K_ATTN_DECODE);
-      launch_attn_decode(qkv, attn, Hq, Hk, kv, da, attn_ws, stream);
+      launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab}, attn, Hq, Hk, kv, da, attn_ws, stream);
       prof_end(K_ATTN_DECODE);
     } else {
       prof_begin(K_ATTN_PREFILL);
@@ -415,7 +451,14 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     const int shapes[5][2] = {{E.QKVN, E.H}, {E.H, E.Hq * E.D}, {2 * E.F, E.H}, {E.H, E.F}, {E.V, E.H}};
     for (auto& sh : shapes) gws = std::max(gws, gemv_workspace_bytes(Md, sh[0], sh[1]));
     E.gemv_ws = E.dalloc<char>(gws, true);
-    E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx));
+    E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
+                                       true);  // zeroed: split-combine tickets
+    E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * ms_engine::kMaxSlabRows * std::max(E.QKVN, E.H));
+    if (const char* v = getenv("MS_SPLIT_QKV")) E.split_qkv = atoi(v);
+    if (const char* v = getenv("MS_ATTN_SLABS")) E.attn_slabs = atoi(v) != 0;
+    if (const char* v = getenv("MS_ATTN_FUSED_COMBINE")) E.attn_fused_combine = atoi(v) != 0;
+    if (const char* v = getenv("MS_SPLIT_O")) E.split_o = atoi(v);
+    if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
@@ -829,10 +872,9 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   E.prof_begin(K_MISC);
   launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
   E.prof_end(K_MISC);
+  E.pending_split = 0;
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
-  E.prof_begin(K_MISC);
-  launch_rmsnorm(E.x, E.final_norm, E.xb, B, E.H, E.cfg.norm_eps, nullptr, E.stream);
-  E.prof_end(K_MISC);
+  E.residual_norm(E.final_norm, B);  // folds the last layer's down slabs (if fused)
   if (E.lmq.ready() && qgemv_supported(B, E.V, E.H, MS_GEMV_EPI_STORE_F32))
     E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_GEMV_EPI_STORE_F32, nullptr, K_LMHEAD);
   else
@@ -1089,6 +1131,28 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
     launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
                    (hipStream_t)stream);
+  });
+}
+
+int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
+                     int32_t S, int32_t waves, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && W && slabs && N >= 16 && S >= 1, MS_EINVAL, "bad gemv_split operands");
+    REQUIRE(gemv_split_supported(M, N, K, S), MS_EINVAL, "gemv_split shape unsupported (M<=64, (K/S)%64==0)");
+    launch_gemv_split((const bf16_t*)X, (const bf16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream);
+  });
+}
+
+int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y,
+                           int32_t rows, int32_t hidden, float eps, void* stream) {
+  return op_guard([&] {
+    REQUIRE(x && w && y && rows >= 1 && hidden >= 4 && hidden % 4 == 0 && hidden <= 8192, MS_EINVAL,
+            "bad residual_rmsnorm shape");
+    REQUIRE(S == 0 || slabs, MS_EINVAL, "slabs missing");
+    REQUIRE(residual_rmsnorm_supported(S, hidden) || (S == 0 && hidden <= 8192), MS_EINVAL,
+            "residual_rmsnorm: S <= 8 and hidden <= 3072 (wider rows: S == 0 only)");
+    launch_residual_rmsnorm(x, slabs, S, (const bf16_t*)w, (bf16_t*)y, rows, hidden, eps,
+                            (hipStream_t)stream);
   });
 }
 

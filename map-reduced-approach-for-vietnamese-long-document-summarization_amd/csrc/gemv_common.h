@@ -6,14 +6,15 @@ namespace ms {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *(const uint4*)p; }
 
-// X rows [M][K] bf16 -> LDS, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of an
-// MFMA fragment read on different banks).  Caller synchronises.
-__device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restrict__ X, int M, int K) {
+// X rows [M][K] bf16 (row stride ldx elements) -> LDS, row stride 2K+16 bytes (the 16-B
+// skew puts the 16 rows of an MFMA fragment read on different banks).  Caller synchronises.
+__device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restrict__ X, int M, int K,
+                                             int ldx) {
   const size_t xstride = 2 * (size_t)K + 16;
   const int kch = K / 8;  // 16-B chunks per row
   for (int c = threadIdx.x; c < M * kch; c += blockDim.x) {
     const int r = c / kch, k8 = c - r * kch;
-    *(uint4*)(smem + r * xstride + k8 * 16) = ldg16(X + (size_t)r * K + k8 * 8);
+    *(uint4*)(smem + r * xstride + k8 * 16) = ldg16(X + (size_t)r * ldx + k8 * 8);
   }
 }
 

@@ -194,20 +194,44 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 // grid (B, Hk, nsplit); block 256 = 4 waves, ONE 64-key page per wave, so a block covers
 // 256 keys and every wave has its whole page (K as MFMA fragments + V rows, 32 KB)
 // in flight before its first MFMA.  The G query heads of the kv head are MFMA columns
-// 0..G-1.  Per-wave (m, l, O^T) are merged in LDS (reusing the wave's V image) and the
-// block writes one partial (m, l, o[128]) per (b, q head, split) for the combine kernel.
+// 0..G-1.  Per-wave (m, l, O^T) are merged in LDS (reusing the waves' V images); each block
+// writes one partial (m, l, o[128]) per (b, q head, split), and the LAST block of a
+// (b, kv head) to finish (agent-scope release/acquire ticket, cdna_hip_programming.md §6
+// Guideline 16) combines the nsplit partials and writes the bf16 output -- no second launch.
+//
+// FROM_SLABS (the fused decode chain): the QKV projection arrives as S fp32 split-K slabs
+// [S][B][(Hq+2Hk)*128] with Q/K rows rope-permuted (k_gemv.hip).  The prologue adds the
+// slabs (slab order), rounds q/k/v to bf16, applies RoPE in fp32 and rounds again -- the
+// arithmetic of rope_kv_kernel -- and the block that owns the new token's page writes its
+// K/V into the cache (for later steps) and patches them into the page it holds in
+// registers / LDS.  Otherwise q comes from bf16 qkv rows already roped (rope_kv_kernel).
 constexpr int kSplitPages = 4;  // = waves per block
+constexpr int kMaxGroup = 8;    // q heads per kv head
+constexpr int kMaxSlabs = 8;    // QKV split-K slabs (engine kMaxSplit)
 
+static int decode_nsplit(int max_len) { return (max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage); }
+
+constexpr int kMaxTickets = 4096;  // (b, kv head) pairs per launch
+constexpr int kMaxSplits = 127;
+
+// workspace: [tickets: kMaxTickets u32, zero at allocation, reset by each last arriver]
+//            [partials: (b, q head, split) x 132 floats]
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
-  const int nsplit = (max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
-  return (size_t)B * Hq * nsplit * 132 * sizeof(float);
+  return (size_t)kMaxTickets * 4 + (size_t)B * Hq * decode_nsplit(max_len) * 132 * sizeof(float);
 }
 
-__global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restrict__ qkv, int Hq,
-                                                          int Hk, KVView kv, DecodeAttnArgs a,
-                                                          float* __restrict__ ws, int nsplit,
+bool attn_decode_supported(int B, int Hq, int Hk, int max_len) {
+  return Hk >= 1 && Hq % Hk == 0 && Hq / Hk <= kMaxGroup && B * Hk <= kMaxTickets &&
+         decode_nsplit(max_len) <= kMaxSplits;
+}
+
+template <bool FROM_SLABS, bool FUSED_COMBINE>
+__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
+                                                          DecodeAttnArgs a, float* __restrict__ ws,
+                                                          unsigned* __restrict__ tickets,
+                                                          bf16_t* __restrict__ out, int nsplit,
                                                           float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * 16384];
+  __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + (kMaxGroup + 2) * kHeadDim * 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int b = blockIdx.x, kvh = blockIdx.y, split = blockIdx.z;
@@ -218,6 +242,78 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   char* vs_ = smem + wave * 16384;
   const int pg = split * kSplitPages + wave;
   const bool active = pg * kPage < len;  // wave-uniform
+  const int pos = len - 1;               // the new token
+  bf16_t* qn = (bf16_t*)(smem + 4 * 16384);  // [G][128] roped q
+  bf16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
+  bf16_t* vn = kn + kHeadDim;                 // [128] v of the new token
+
+  // issue the whole page first -- K fragments (16 rows x 64 B per instruction) and V rows
+  // (1 KB) -- so its HBM latency overlaps the q/k/v prologue
+  u32x4 kf[4][4], vr[16];
+  if (active) {
+    const size_t base =
+        ((size_t)kv.block_table[(size_t)slot * kv.max_pages + pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        kf[mt][s4] = *(const u32x4*)(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      vr[i] = *(const u32x4*)(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
+  }
+
+  if constexpr (FROM_SLABS) {
+    const bool owns_new = (pos / kPage) / kSplitPages == split;  // block-uniform
+    float* raw = (float*)smem;  // [(G+2)][128] bf16-rounded sums; aliases wave 0's V image
+    const size_t sstride = (size_t)a.B * row_stride;
+    const float* src = qa.slabs + (size_t)b * row_stride;
+    const float rcs = qa.cos_tab[(size_t)pos * 64 + (tid & 63)];  // this thread's rope pair i
+    const float rsn = qa.sin_tab[(size_t)pos * 64 + (tid & 63)];
+    const int nvec = (G + (owns_new ? 2 : 0)) * kHeadDim;
+    constexpr int PER = ((kMaxGroup + 2) * kHeadDim + 255) / 256;
+    float sv[PER][kMaxSlabs];  // every slab load of this thread in flight at once
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i * 256 >= nvec) break;  // block-uniform
+      const int e = min(tid + i * 256, nvec - 1);
+      const int hh = e >> 7, j = e & 127;  // hh < G: q head kvh*G+hh; G: k; G+1: v
+      const int col = hh < G ? (kvh * G + hh) * kHeadDim + j
+                             : (hh == G ? (Hq + kvh) * kHeadDim + j : (Hq + Hk + kvh) * kHeadDim + j);
+#pragma unroll
+      for (int q = 0; q < kMaxSlabs; ++q) sv[i][q] = src[min(q, qa.S - 1) * sstride + col];
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + i * 256;
+      if (i * 256 >= nvec) break;
+      float acc = sv[i][0];
+#pragma unroll
+      for (int q = 1; q < kMaxSlabs; ++q)
+        if (q < qa.S) acc += sv[i][q];
+      if (e < nvec) raw[e] = bf2f(f2bf(acc));
+    }
+    __syncthreads();
+    const int nrot = (G + (owns_new ? 1 : 0)) * 64;  // (head, i) pairs: the q heads, then k
+    for (int e = tid; e < nrot; e += 256) {
+      const int hh = e >> 6, i = e & 63;  // i == tid & 63 for every e of this thread
+      const float lo = raw[hh * kHeadDim + rope_perm(i)], hi = raw[hh * kHeadDim + rope_perm(64 + i)];
+      const float cs = rcs, sn = rsn;
+      const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
+      const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
+      bf16_t* dst = hh < G ? qn + hh * kHeadDim : kn;
+      dst[i] = f2bf(ra);
+      dst[64 + i] = f2bf(rb);
+    }
+    if (owns_new && tid < kHeadDim) vn[tid] = f2bf(raw[(G + 1) * kHeadDim + tid]);
+    __syncthreads();  // raw consumed (wave 0 may stage V); qn/kn/vn ready
+    if (owns_new && tid < kHeadDim) {  // the new token's K/V into the cache, for later steps
+      const int page = kv.block_table[(size_t)slot * kv.max_pages + pos / kPage];
+      const size_t o = (((size_t)page * kv.n_kv_heads + kvh) * kPage + pos % kPage) * kHeadDim + tid;
+      kv.k[o] = kn[tid];
+      kv.v[o] = vn[tid];
+    }
+  }
 
   f32x4 o[8];
 #pragma unroll
@@ -225,31 +321,33 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
   float m_run = -INFINITY, l_run = 0.f;
 
   if (active) {
-    const size_t base =
-        ((size_t)kv.block_table[(size_t)slot * kv.max_pages + pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
-    // issue the whole page: K fragments (16 rows x 64 B per instruction) and V rows (1 KB)
-    u32x4 kf[4][4], vr[16];
-#pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        kf[mt][s] = *(const u32x4*)(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s + 8 * g);
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-      vr[i] = *(const u32x4*)(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
     bf16x8 qf[4];
     {
-      const int hq = kvh * G + min(r, G - 1);
-      const bf16_t* qrow = qkv + (size_t)b * row_stride + hq * kHeadDim;
+      const int hl = min(r, G - 1);
+      if constexpr (FROM_SLABS) {
 #pragma unroll
-      for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
+        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const bf16x8*)(qn + hl * kHeadDim + 32 * s4 + 8 * g);
+      } else {
+        const bf16_t* qrow = qa.qkv + (size_t)b * row_stride + (kvh * G + hl) * kHeadDim;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = as_bf16x8(*(const uint4*)(qrow + 32 * s4 + 8 * g));
+      }
+    }
+    const bool patch = FROM_SLABS && pg == pos / kPage;  // wave-uniform: holds the new token
+    const int off = pos % kPage;
+    if (patch) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          if (mt * 16 + r == off) kf[mt][s4] = *(const u32x4*)(kn + 32 * s4 + 8 * g);
     }
     f32x4 sc[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
       sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s]), qf[s], sc[mt]);
+      for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
     }
     float mx = -INFINITY;
 #pragma unroll
@@ -281,6 +379,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     for (int i = 0; i < 16; ++i) {
       const int row = i * 4 + (lane >> 4);
       if (pg * kPage + row >= len) vr[i] = u32x4{0, 0, 0, 0};
+      if (patch && row == off) vr[i] = *(const u32x4*)(vn + (lane & 15) * 8);
       *(u32x4*)(vs_ + v_swz(row, lane & 15)) = vr[i];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the V image is in LDS
@@ -321,9 +420,71 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(const bf16_t* __restri
     float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;
     dst[k] = (k == 0) ? M : acc;
   }
+
+  // ---- in-launch combine: the last of the nsplit blocks of (b, kvh) merges the partials
+  if constexpr (!FUSED_COMBINE) return;
+  wait_vmcnt0();    // every storing wave: its partial stores have completed
+  __syncthreads();
+  unsigned* flag = (unsigned*)(smem + 4 * 16384);  // reuse qn (consumed)
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    wait_vmcnt0();
+    const unsigned t = __hip_atomic_fetch_add(&tickets[b * Hk + kvh], 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == (unsigned)nsplit - 1;
+    if (last) {
+      __hip_atomic_store(&tickets[b * Hk + kvh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      wait_vmcnt0();
+    }
+    *flag = last ? 1u : 0u;
+  }
+  __syncthreads();
+  if (*flag == 0u) return;
+  // split weights per q head: f_s = 2^(m_s - max m), L = sum_s f_s l_s (split order)
+  float* ml = (float*)smem;                           // [G][128] m_s, then [G][128] l_s
+  float* wsum = ml + 2 * kMaxGroup * 128;             // [G][128] f_s, [c][127] = L
+  for (int e = tid; e < G * nsplit; e += 256) {       // every (head, split) load in parallel
+    const int c = e / nsplit, s_ = e - c * nsplit;
+    const float* p = ws + (((size_t)b * Hq + kvh * G + c) * nsplit + s_) * 132;
+    ml[c * 128 + s_] = p[0];
+    ml[(kMaxGroup + c) * 128 + s_] = p[1];
+  }
+  __syncthreads();
+  for (int c = tid; c < G; c += 256) {
+    float M = -INFINITY;
+    for (int s_ = 0; s_ < nsplit; ++s_) M = fmaxf(M, ml[c * 128 + s_]);
+    float L = 0.f;
+    for (int s_ = 0; s_ < nsplit; ++s_) {
+      const float ms_ = ml[c * 128 + s_];
+      const float f = (ms_ == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ms_ - M);
+      wsum[c * 128 + s_] = f;
+      L += f * ml[(kMaxGroup + c) * 128 + s_];
+    }
+    wsum[c * 128 + 127] = L;
+  }
+  __syncthreads();
+  for (int e = tid; e < G * kHeadDim; e += 256) {
+    const int c = e >> 7, d = e & 127;
+    const float* p = ws + ((size_t)b * Hq + kvh * G + c) * nsplit * 132 + 2 + d;
+    const float* f = wsum + c * 128;
+    float O = 0.f;
+    if (nsplit <= 16) {  // clamped indices, no branches: all loads in flight at once
+      float ov[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) ov[q] = p[min(q, nsplit - 1) * 132];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) O += (q < nsplit) ? f[q] * ov[q] : 0.f;
+    } else {
+      for (int q = 0; q < nsplit; ++q) O += f[q] * p[q * 132];
+    }
+    out[(size_t)b * Hq * kHeadDim + (kvh * G + c) * kHeadDim + d] = f2bf(O / f[127]);
+  }
 }
 
-// out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s,  w_s = 2^(m_s - max m)
+// separate split combine (the default): out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s,
+// w_s = 2^(m_s - max m) -- measured cheaper on MI355X than the in-launch ticket combine,
+// whose release/acquire chain adds ~4 dependent memory round trips to every block
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
                                                                   bf16_t* __restrict__ out, int Hq,
                                                                   int nsplit) {
@@ -342,15 +503,26 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
   out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2bf(O / L);
 }
 
-void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
-                        DecodeAttnArgs a, float* ws, hipStream_t s) {
+void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
+                        DecodeAttnArgs a, float* ws, hipStream_t s, bool fused_combine) {
   if (a.B <= 0) return;
-  const int nsplit = (a.max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage);
+  if (!attn_decode_supported(a.B, Hq, Hk, a.max_len)) return;  // callers check
+  if (qa.slabs && (qa.S < 1 || qa.S > kMaxSlabs)) return;
+  const int nsplit = decode_nsplit(a.max_len);
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
-  MS_LAUNCH(attn_decode_kernel, dim3(a.B, Hk, nsplit), dim3(256), 0, s, qkv, Hq, Hk, kv,
-                     a, ws, nsplit, scale_log2);
-  MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq,
-                     nsplit);
+  unsigned* tickets = (unsigned*)ws;
+  ws = (float*)((char*)ws + (size_t)kMaxTickets * 4);
+  const dim3 grid(a.B, Hk, nsplit);
+#define AD(SL, FC)                                                                                   \
+  MS_LAUNCH((attn_decode_kernel<SL, FC>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
+            nsplit, scale_log2)
+  if (qa.slabs && fused_combine) AD(true, true);
+  else if (qa.slabs) AD(true, false);
+  else if (fused_combine) AD(false, true);
+  else AD(false, false);
+#undef AD
+  if (!fused_combine)
+    MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
 }
 
 }  // namespace ms

@@ -63,22 +63,30 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
   return xs > red ? xs : red;
 }
 
+// Split-K (gridDim.y = S > 1, STORE_F32 only): block (x, y) covers k in [y*K, (y+1)*K) of
+// rows of length ldk and writes its fp32 partial to slab y = out + y*M*ldo; the consumer
+// (residual_rmsnorm_kernel) adds the S slabs in slab order -- deterministic, no atomics.
 template <int MT, int NT, int EPI, int U, bool XL>
 __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
-                                                    int ldo, GemvArgs ga) {
+                                                    int ldk, int ldo, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
   const int kbeg = wave * U * 64;
+  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
+    X += (size_t)blockIdx.y * K;
+    W += (size_t)blockIdx.y * K;
+    out = (float*)out + (size_t)blockIdx.y * M * ldo;
+  }
 
   // 1. issue this wave's whole W stream first (HBM latency overlaps the X staging)
   uint4 w[U][NT][2];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const bf16_t* wp = W + (size_t)min(n0 + n * 16 + fr, N - 1) * K + kbeg + 16 * fg;
+    const bf16_t* wp = W + (size_t)min(n0 + n * 16 + fr, N - 1) * ldk + kbeg + 16 * fg;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       w[u][n][0] = ldg16(wp + u * 64);
@@ -88,7 +96,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
   // 2. stage the M rows of X into LDS (XL) -- or read fragments from L2 (large M*K)
   const size_t xstride = 2 * (size_t)K + 16;
   if constexpr (XL) {
-    gemv_stage_x(smem, X, M, K);
+    gemv_stage_x(smem, X, M, K, ldk);
     __syncthreads();
   }
 
@@ -108,7 +116,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
         x0 = *(const bf16x8*)xr;
         x1 = *(const bf16x8*)(xr + 16);
       } else {
-        const bf16_t* xg = X + (size_t)xrow * K + kbeg + u * 64 + 16 * fg;
+        const bf16_t* xg = X + (size_t)xrow * ldk + kbeg + u * 64 + 16 * fg;
         x0 = as_bf16x8(ldg16(xg));
         x1 = as_bf16x8(ldg16(xg + 8));
       }
@@ -123,27 +131,27 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 }
 
 template <int MT, int NT, int EPI, int U>
-static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                    const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                    int S, int ldo, const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
                     hipStream_t s) {
-  const dim3 grid(p.tiles), blk(64 * p.waves);
+  const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
     if (xl)
       MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M,
-                         N, K, ldo, ga);
+                         N, K, ldk, ldo, ga);
     else
       MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out,
-                         M, N, K, ldo, ga);
+                         M, N, K, ldk, ldo, ga);
   }
 }
 
 template <int MT, int NT, int EPI>
-static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                      const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                      int S, int ldo, const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
                       hipStream_t s) {
-#define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldo, p, lds, xl, ga, s)
+#define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xl, ga, s)
   switch (p.U) {
     case 1: GU(1); break;
     case 2: GU(2); break;
@@ -158,10 +166,10 @@ static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N,
 }
 
 template <int MT>
-static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                       int epi, const GemvPlan& p, size_t lds, bool xl,
+static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                       int S, int ldo, int epi, const GemvPlan& p, size_t lds, bool xl,
                        const GemvArgs& ga, hipStream_t s) {
-#define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldo, p, lds, xl, ga, s)
+#define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xl, ga, s)
   switch (epi) {
     case MS_GEMV_EPI_STORE_BF16: GE(1, MS_GEMV_EPI_STORE_BF16); break;
     case MS_GEMV_EPI_ADD_F32: GE(1, MS_GEMV_EPI_ADD_F32); break;
@@ -181,8 +189,9 @@ bool gemv_supported(int M, int N, int K, int epi) {
   return gemv_lds_bytes(p, M, K, false) <= kMaxLds;
 }
 
-void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                    int epi, const GemvArgs* ga_in, int force_waves, hipStream_t s) {
+static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                          int S, int ldo, int epi, const GemvArgs* ga_in, int force_waves,
+                          hipStream_t s) {
   if (M <= 0) return;
   const GemvPlan p = gemv_plan(M, N, K, epi, force_waves);
   if (p.waves == 0) return;  // callers check gemv_supported()
@@ -192,11 +201,26 @@ void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
   switch (p.MT) {
-    case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
-    case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
-    case 3: gemv_go_mt<3>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
-    default: gemv_go_mt<4>(X, W, out, M, N, K, ldo, epi, p, lds, xl, ga, s); break;
+    case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
+    case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
+    case 3: gemv_go_mt<3>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
+    default: gemv_go_mt<4>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
   }
+}
+
+void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+                    int epi, const GemvArgs* ga_in, int force_waves, hipStream_t s) {
+  gemv_dispatch(X, W, out, M, N, K, K, 1, ldo, epi, ga_in, force_waves, s);
+}
+
+bool gemv_split_supported(int M, int N, int K, int S) {
+  if (S < 1 || K % S) return false;
+  return gemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32);
+}
+
+void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
+                       int force_waves, hipStream_t s) {
+  gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, nullptr, force_waves, s);
 }
 
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,

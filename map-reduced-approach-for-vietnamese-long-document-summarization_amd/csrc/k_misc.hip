@@ -82,6 +82,87 @@ void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H,
   MS_LAUNCH(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, H, eps, row_idx);
 }
 
+// Decode: the residual update of a split-K projection fused with the next RMSNorm.
+// x[r] += (slab_0[r] + slab_1[r] + ... + slab_{S-1}[r]), then y[r] = bf16((x[r]*rinv)*w).
+// The summation order is fixed (slab order), so the result does not depend on timing or on
+// the other rows.  One block per row; every load (x, w, all S slabs) is issued before the
+// first add (S is a template parameter: a runtime trip count serialises the loads).
+template <int S>
+__global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict__ x,
+                                                               const float* __restrict__ slabs,
+                                                               int rows,
+                                                               const bf16_t* __restrict__ w,
+                                                               bf16_t* __restrict__ y, int H,
+                                                               float eps) {
+  constexpr int KMAX = 3;  // float4 per thread: H <= 3072
+  __shared__ float red[4];
+  const int r = blockIdx.x;
+  float* xr = x + (size_t)r * H;
+  const int n4 = H / 4;
+  const size_t slab = (size_t)rows * H;
+  float4 v[KMAX], p[KMAX][S > 0 ? S : 1];
+  uint2 wv[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int c = min((int)threadIdx.x + k * 256, n4 - 1);
+    v[k] = *(const float4*)(xr + c * 4);
+    wv[k] = *(const uint2*)(w + c * 4);
+#pragma unroll
+    for (int q = 0; q < S; ++q) p[k][q] = *(const float4*)(slabs + q * slab + (size_t)r * H + c * 4);
+  }
+  if constexpr (S > 0) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      float4 a = p[k][0];
+#pragma unroll
+      for (int q = 1; q < S; ++q) {
+        a.x += p[k][q].x; a.y += p[k][q].y; a.z += p[k][q].z; a.w += p[k][q].w;
+      }
+      v[k].x += a.x; v[k].y += a.y; v[k].z += a.z; v[k].w += a.w;
+      const int c = threadIdx.x + k * 256;
+      if (c < n4) *(float4*)(xr + c * 4) = v[k];
+    }
+  }
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float rinv = 1.0f / sqrtf(tot / (float)H + eps);
+  bf16_t* yr = y + (size_t)r * H;
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    const int c = threadIdx.x + k * 256;
+    if (c >= n4) break;
+    const float g0 = __uint_as_float(wv[k].x << 16), g1 = __uint_as_float(wv[k].x & 0xFFFF0000u);
+    const float g2 = __uint_as_float(wv[k].y << 16), g3 = __uint_as_float(wv[k].y & 0xFFFF0000u);
+    uint2 o;
+    o.x = pack2bf((v[k].x * rinv) * g0, (v[k].y * rinv) * g1);
+    o.y = pack2bf((v[k].z * rinv) * g2, (v[k].w * rinv) * g3);
+    *(uint2*)(yr + c * 4) = o;
+  }
+}
+
+bool residual_rmsnorm_supported(int S, int H) { return S >= 0 && S <= 8 && H % 4 == 0 && H <= 3072; }
+
+void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
+                             int rows, int H, float eps, hipStream_t s) {
+  if (rows <= 0) return;
+  if (H > 3072) {  // wider models: the plain kernel (S = 0 only)
+    launch_rmsnorm(x, w, y, rows, H, eps, nullptr, s);
+    return;
+  }
+#define RN(S_)                                                                                 \
+  case S_:                                                                                     \
+    MS_LAUNCH(residual_rmsnorm_kernel<S_>, dim3(rows), dim3(256), 0, s, x, slabs, rows, w, y, H, eps); \
+    break;
+  switch (S) { RN(0) RN(1) RN(2) RN(3) RN(4) RN(5) RN(6) RN(7) RN(8) }
+#undef RN
+}
+
 // ---------------------------------------------------------------- RoPE + KV scatter
 // qkv row layout: [Q heads | K heads | V heads] x 128, Q/K heads rope-permuted (the fused
 // weight rows are uploaded in rope_perm order so a 16-row GEMV tile holds dims i and i+64).

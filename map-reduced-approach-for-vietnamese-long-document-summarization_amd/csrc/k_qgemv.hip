@@ -193,7 +193,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         q1[j][n] = ldg16(bp + 32 + 32 * g);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K);
+      gemv_stage_x(smem, X, M, K, K);
       __syncthreads();
     }
 #pragma unroll
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K);
+      gemv_stage_x(smem, X, M, K, K);
       __syncthreads();
     }
 #pragma unroll

@@ -61,6 +61,16 @@ struct GemvArgs {
   KVView kv;
   int Hq, Hk;
 };
+// split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
+// consumer adds them in slab order (launch_residual_rmsnorm)
+bool gemv_split_supported(int M, int N, int K, int S);
+void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
+                       int force_waves, hipStream_t s);
+// x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = RMSNorm(x)*w.
+// S = 0: plain RMSNorm.  Supported: S <= 8, H <= 3072 (H > 3072 only with S = 0).
+bool residual_rmsnorm_supported(int S, int H);
+void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
+                             int rows, int H, float eps, hipStream_t s);
 size_t gemv_workspace_bytes(int M, int N, int K);
 bool gemv_supported(int M, int N, int K, int epi);
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
@@ -102,9 +112,21 @@ void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K
 
 void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s);
+// decode attention input: either bf16 qkv rows already roped with K/V in the cache
+// (slabs == nullptr), or S fp32 split-K slabs of the QKV projection (rope-permuted Q/K rows):
+// the kernel then adds the slabs, applies RoPE and writes the new token's K/V itself.
+struct DecodeQKV {
+  const bf16_t* qkv;
+  const float* slabs;
+  int S;
+  const float* cos_tab;
+  const float* sin_tab;
+};
+// workspace must be zero-filled once at allocation (split-combine tickets live there)
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len);
-void launch_attn_decode(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
-                        DecodeAttnArgs a, float* ws, hipStream_t s);
+bool attn_decode_supported(int B, int Hq, int Hk, int max_len);
+void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
+                        DecodeAttnArgs a, float* ws, hipStream_t s, bool fused_combine = false);
 
 // synthetic weights (oracle/synth.py restates this generator)
 // row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the

@@ -67,6 +67,34 @@ def bench_gemv(lib, M, shapes, waves_list):
         print(line, flush=True)
 
 
+def bench_split(lib, M):
+    """Split-K decode GEMV into fp32 slabs (O / down projections) over (S, waves)."""
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, N, K in [("o", 3072, 3072), ("down", 3072, 8192), ("qkv", 5120, 3072)]:
+        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02 for _ in range(8)]
+        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        slabs = torch.zeros(8, M, N, device=dev)
+        for S in (1, 2, 3, 4, 6, 8):
+            byts = N * K * 2 + M * K * 2 + S * M * N * 4
+            line = f"{name:5s} N={N:5d} K={K:5d} M={M:2d} S={S} |"
+            for wv in (0, 2, 4, 8, 12, 16):
+                i = [0]
+
+                def fn():
+                    W = Ws[i[0] % len(Ws)]
+                    i[0] += 1
+                    rc = lib.ms_op_gemv_split(X.data_ptr(), W.data_ptr(), slabs.data_ptr(), M, N, K, S, wv, st)
+                    if rc:
+                        raise RuntimeError(lib.ms_last_error(None))
+                try:
+                    t = timeit(fn)
+                    line += f" w{wv}: {t*1e3:6.1f}us {byts/t/1e6:5.0f} |"
+                except RuntimeError:
+                    line += f" w{wv}: n/a |"
+            print(line, flush=True)
+
+
 def bench_gemm(lib):
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -87,7 +115,7 @@ def bench_gemm(lib):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split"])
     ap.add_argument("--m", type=int, default=8)
     a = ap.parse_args()
     lib = L.load()
@@ -95,5 +123,7 @@ if __name__ == "__main__":
         shapes = [("qkv", 5120, 3072, 0), ("o", 3072, 3072, 1), ("gu", 16384, 3072, 2),
                   ("down", 3072, 8192, 1), ("lm_head", 128256, 3072, 3)]
         bench_gemv(lib, a.m, shapes, [0, 6, 8, 12, 16])
+    elif a.what == "split":
+        bench_split(lib, a.m)
     else:
         bench_gemm(lib)
