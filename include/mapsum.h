@@ -164,6 +164,8 @@ int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run
 /* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0 */
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* stream);
+/* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase) */
+int ms_set_gemm_variant(int32_t variant);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,

@@ -1113,6 +1113,12 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
   });
 }
 
+int ms_set_gemm_variant(int32_t v) {
+  if (v < 0 || v > 2) return MS_EINVAL;
+  set_gemm_variant(v);
+  return MS_OK;
+}
+
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K) {
   if (M < 1 || M > 64 || N < 16 || K < 64 || K % 64) return MS_EINVAL;
   return (int64_t)gemv_workspace_bytes(M, N, K);

@@ -137,9 +137,214 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------ 256x256 8-phase tile
+// The large-M prefill shapes (M = packed prompt tokens, thousands) run a 256x256x64 tile,
+// 512 threads = 8 waves in 2 (M) x 4 (N), each wave a 128x64 output = 8x4 MFMA tiles
+// (cdna_hip_programming.md §5 "The 256² 8-phase template"; our own schedule below).
+// LDS: two K-tile buffers of 64 KiB (A image [256][128 B], B image [256][128 B]), filled
+// by global_load_lds in 16-KiB "units" of 128 rows:
+//   UAt = A rows {0..63, 128..191}   UAb = A rows {64..127, 192..255}
+//   UBl = B rows {64w + 0..31}       UBr = B rows {64w + 32..63}   (w = 0..3)
+// A K-tile is computed in 4 phases, one C quadrant each (wave-local 64x32):
+//   phase 0: ds-read A top    + B left  -> MFMA (top, left)
+//   phase 1: ds-read B right            -> MFMA (top, right)
+//   phase 2: ds-read A bottom           -> MFMA (bottom, right)
+//   phase 3: ds-read B left             -> MFMA (bottom, left)
+// so UAt is last read in phase 0, UBr in 1, UAb in 2, UBl in 3.  A unit may be restaged
+// two phases after its last read, and each phase issues exactly one unit:
+//   phase 0: UAb(t+1)  phase 1: UBl(t+1)  phase 2: UAt(t+2)  phase 3: UBr(t+2)
+// then phase 3 waits vmcnt(4): everything up to UBl(t+1) has landed while UAt/UBr(t+2)
+// stay in flight across the barrier (never vmcnt(0) in the steady state).  Tile t+1 is
+// first read in the next phase, after a barrier.  The two wave rows run one barrier apart
+// (wave row 1 takes an extra s_barrier up front), so one row's MFMA cluster overlaps the
+// other row's LDS reads and DMA issue.  LDS swizzle: row r holds global 16-B chunk
+// c ^ ((r >> 1) & 7) at chunk c -- the 16 rows of a fragment read hit 16 distinct slots of
+// the 256-B bank window (conflict-free); applied on the DMA source and on the read.
+constexpr int TBM = 256, TBN = 256, TBK = 64;
+
+__device__ __forceinline__ int swz2(int r) { return (r >> 1) & 7; }
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A,
+                                                        const bf16_t* __restrict__ W,
+                                                        void* __restrict__ out, int M, int N, int K,
+                                                        int ldo) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (N + TBN - 1) / TBN;
+  const int pid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int grp = pid / (GM * tiles_n);
+  const int first_m = grp * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int in_grp = pid % (GM * tiles_n);
+  const int tm = first_m + in_grp % gsz, tn = in_grp / gsz;
+  const int m0 = tm * TBM, n0 = tn * TBN;
+
+  // DMA sources: unit u, instruction i -> local row lr = (2*wave + i)*8 + lane/8
+  uint32_t src_off[4][2];
+  int dst_row[4][2];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int lr = (2 * wave + i) * 8 + (lane >> 3);
+      int tr;
+      if (u == 0) tr = lr < 64 ? lr : lr + 64;
+      else if (u == 1) tr = lr < 64 ? lr + 64 : lr + 128;
+      else tr = (lr >> 5) * 64 + (lr & 31) + (u == 3 ? 32 : 0);
+      const int grow = u < 2 ? min(m0 + tr, M - 1) : min(n0 + tr, N - 1);
+      src_off[u][i] = (uint32_t)grow * (uint32_t)K + (uint32_t)(((lane & 7) ^ swz2(tr)) * 8);
+      dst_row[u][i] = tr - (lane >> 3);  // first row of the instruction's 8-row group
+    }
+  auto stage = [&](int buf, int u, int k0) {
+    const bf16_t* base = u < 2 ? A : W;
+    char* img = smem + buf * 65536 + (u < 2 ? 0 : 32768);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(base + src_off[u][i] + k0),
+                                       (LDS_AS void*)(img + dst_row[u][i] * 128), 16, 0, 0);
+  };
+
+  const int wr = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int sw = fr >> 1;  // swz2(row) for every fragment row (rows = 16-aligned base + fr)
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], bfr[2][2];
+
+  auto read_a = [&](int buf, int qa) {
+    const char* img = smem + buf * 65536;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = wr * 128 + qa * 64 + m * 16 + fr;
+        af[m][s2] = *(const bf16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
+      }
+  };
+  auto read_b = [&](int buf, int qb) {
+    const char* img = smem + buf * 65536 + 32768;
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int row = wc * 64 + qb * 32 + n * 16 + fr;
+        bfr[n][s2] = *(const bf16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
+      }
+  };
+  auto mma = [&](int qa, int qb) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+          acc[qa * 4 + m][qb * 2 + n] = mfma16(af[m][s2], bfr[n][s2], acc[qa * 4 + m][qb * 2 + n]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  const int nk = K / TBK;
+  // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
+  stage(0, 0, 0);
+  stage(0, 3, 0);
+  stage(0, 1, 0);
+  stage(0, 2, 0);
+  if (nk > 1) {
+    stage(1, 0, TBK);
+    stage(1, 3, TBK);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the two wave rows by one barrier
+
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1, nb = buf ^ 1;
+    const bool has1 = t + 1 < nk, has2 = t + 2 < nk;
+    // phase 0
+    read_b(buf, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_a(buf, 0);
+    if (has1) stage(nb, 1, (t + 1) * TBK);
+    mma(0, 0);
+    // phase 1
+    read_b(buf, 1);
+    if (has1) stage(nb, 2, (t + 1) * TBK);
+    mma(0, 1);
+    // phase 2
+    read_a(buf, 1);
+    if (has2) stage(buf, 0, (t + 2) * TBK);
+    mma(1, 1);
+    // phase 3
+    read_b(buf, 0);
+    if (has2) {
+      stage(buf, 3, (t + 2) * TBK);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    mma(1, 0);
+  }
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
+
+  // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x64
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
+      if (row >= M) continue;
+      if constexpr (EPI == 2) {  // SwiGLU: ni even = gate, ni odd = up of the same 16 features
+#pragma unroll
+        for (int ni = 0; ni < 4; ni += 2) {
+          const int col = n0 + wc * 64 + ni * 16;  // multiple of 32
+          if (col >= N) continue;
+          const int f = (col >> 5) * 16 + fr;
+          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[mi][ni][j], acc[mi][ni + 1][j]));
+        }
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int col = n0 + wc * 64 + ni * 16 + fr;
+          if (col >= N) continue;
+          const size_t o = (size_t)row * ldo + col;
+          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[mi][ni][j]);
+          else if constexpr (EPI == 1) ((float*)out)[o] += acc[mi][ni][j];
+          else ((float*)out)[o] = acc[mi][ni][j];
+        }
+      }
+    }
+  }
+}
+
+static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning / tests)
+
+void set_gemm_variant(int v) { g_gemm_variant = v; }
+
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  hipStream_t s) {
   if (M <= 0) return;
+  const bool big = g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
+  if (big) {
+    const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+    switch (epi) {
+      case 0: MS_LAUNCH(gemm256_kernel<0>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
+      case 1: MS_LAUNCH(gemm256_kernel<1>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
+      case 2: MS_LAUNCH(gemm256_kernel<2>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
+      default: MS_LAUNCH(gemm256_kernel<3>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
+    }
+    return;
+  }
   const int grid = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   switch (epi) {
     case 0: MS_LAUNCH(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;

@@ -43,6 +43,8 @@ void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream
 // out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, hipStream_t s);
+// tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
+void set_gemm_variant(int v);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {

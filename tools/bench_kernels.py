@@ -109,8 +109,12 @@ def bench_gemm(lib):
 
         def fn():
             lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st)
-        t = timeit(fn, reps=5, rounds=3)
-        print(f"gemm {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s", flush=True)
+        for variant in (1, 2):
+            lib.ms_set_gemm_variant(variant)
+            t = timeit(fn, reps=5, rounds=3)
+            print(f"gemm v{variant} {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s",
+                  flush=True)
+        lib.ms_set_gemm_variant(0)
 
 
 if __name__ == "__main__":
