@@ -135,6 +135,19 @@ def cpu_baseline(cfg, prompt_len, gen_len, decode_sample=16):
                        f"scaled to {cfg.n_layers} layers x {gen_len} tokens")}
 
 
+def pmc_traffic(weights):
+    """HBM bytes per GEMV launch from the committed rocprofv3 --pmc passes of this same
+    workload (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic_from_pmc.py, run by
+    tools/gpu_round.sh); None when no such measurement is committed.  PMC counters cannot
+    be read from inside a timed run, so this is the profiler's number, not a live one."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                         "profiles", "r*", f"pmc_traffic_{weights}.json")))
+    if not hits:
+        return None
+    return json.load(open(hits[-1]))["traffic_bytes_per_launch"]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,7 +237,7 @@ def main():
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.weights),
                     "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
                               + " decode QKV/O/gate-up/down projections)",
                     "bytes_per_launch": int(bytes_total / launches),

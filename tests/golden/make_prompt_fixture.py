@@ -1,7 +1,8 @@
 """Generate tests/golden/prompts.json: SHA-256 of the reference's map-prompt strings.
 
 Reads the reference runners as TEXT (ast string constants; nothing is imported or run)
-and records the digest of the exact map-prompt constant each runner formats per chunk,
+and records the digest of the exact map-prompt constant each runner formats per chunk (and the map-reduce
+runner's reduce prompt),
 so tests/test_host.py can check mapsum/template.py byte for byte without the
 reference being present (it is absent on the GPU box).
 """
@@ -14,7 +15,9 @@ REF = "/root/reference/runners"
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = {"mapreduce": ("run_summarization_ollama_mapreduce.py", "Vui lòng viết một bản tóm tắt chi tiết cho đoạn"),
        "mapreduce_critique": ("run_summarization_ollama_mapreduce_critique.py", "Văn bản:\n<content>"),
-       "mapreduce_hierarchical": ("run_summarization_ollama_mapreduce_hierarchical.py", "<content>\n{content}\n\n</content>")}
+       "mapreduce_hierarchical": ("run_summarization_ollama_mapreduce_hierarchical.py", "<content>\n{content}\n\n</content>"),
+       # the reduce prompt of the map-reduce graph (mapreduce.py:88-94), for mapsum/mapreduce.py
+       "reduce_mapreduce": ("run_summarization_ollama_mapreduce.py", "Sau đây là một tập hợp các bản tóm tắt:\n{docs}")}
 
 
 def main():
