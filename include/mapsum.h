@@ -188,6 +188,10 @@ int ms_op_quant_rows(int32_t ggml_type, const void* blocks, int32_t rows, int32_
                      void* packed_out, void* stream);
 int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void* out, int32_t M,
                 int32_t N, int32_t K, int32_t ldo, int32_t epilogue, void* stream);
+/* dequant-fused split-K: slabs fp32 [S][M][N] over S equal, super-block aligned K ranges
+   (the quantised counterpart of ms_op_gemv_split; K % (256*S) == 0) */
+int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows, float* slabs,
+                      int32_t M, int32_t N, int32_t K, int32_t S, void* stream);
 /* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
                   const int32_t* row_idx, void* stream);

@@ -111,6 +111,7 @@ struct ms_engine {
   // residual by the next residual_rmsnorm launch (pending_split = S of the unfolded slabs)
   float* slabs = nullptr;
   int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
+  int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
   // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
   bool attn_slabs = true, attn_fused_combine = false;
@@ -223,7 +224,15 @@ struct ms_engine {
     prof_begin(K_GEMV);
     int used = 1;
     if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
-      launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
+      // Q4_K/Q6_K: same split-K as bf16 (a 16-row tile carries 3.6x fewer weight bytes, so
+      // the unsplit grid -- 192 blocks for O/down -- is too thin to cover 256 CUs)
+      const int Sq = qsplit > 0 ? qsplit : S;
+      if (Sq > 1 && Sq <= kMaxSplit && qgemv_split_supported(M, N, K, Sq)) {
+        launch_qgemv_split(X, q->m, slabs, M, N, K, Sq, stream);
+        used = Sq;
+      } else {
+        launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
+      }
     } else {
       if (!(S >= 1 && S <= kMaxSplit && gemv_split_supported(M, N, K, S))) S = 1;
       launch_gemv_split(X, W, slabs, M, N, K, S, 0, stream);
@@ -459,6 +468,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_ATTN_FUSED_COMBINE")) E.attn_fused_combine = atoi(v) != 0;
     if (const char* v = getenv("MS_SPLIT_O")) E.split_o = atoi(v);
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
+    if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
@@ -1194,6 +1204,22 @@ int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int3
     q.type0 = type;
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
     launch_qgemv((const bf16_t*)X, q, out, M, N, K, ldo, epi, nullptr, (hipStream_t)stream);
+  });
+}
+
+int ms_op_qgemv_split(const void* X, int32_t type, const void* packed, float* slabs, int32_t M,
+                      int32_t N, int32_t K, int32_t S, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && packed && slabs && N >= 16 && S >= 1, MS_EINVAL, "bad qgemv_split operands");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    REQUIRE(qgemv_split_supported(M, N, K, S), MS_EINVAL, "qgemv_split shape unsupported (M<=64, K%(256*S)==0)");
+    QMat q{};
+    q.n = 1;
+    q.base0 = (const uint8_t*)packed;
+    q.row0_0 = 0;
+    q.type0 = type;
+    q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
+    launch_qgemv_split((const bf16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream);
   });
 }
 

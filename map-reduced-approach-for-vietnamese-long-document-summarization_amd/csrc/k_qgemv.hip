@@ -164,6 +164,13 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
+  // of the full row, where K is the per-split length; X and out shift to that slab.
+  const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
+  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
+    X += (size_t)blockIdx.y * K;
+    out = (float*)out + (size_t)blockIdx.y * M * ldo;
+  }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
@@ -187,13 +194,13 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sb0 + j) * kQ4KBytes;
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ4KBytes;
         hq[j][n] = ldg16(bp);
         q0[j][n] = ldg16(bp + 16 + 32 * g);
         q1[j][n] = ldg16(bp + 32 + 32 * g);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K, K);
+      gemv_stage_x(smem, X, M, K, ldx);
       __syncthreads();
     }
 #pragma unroll
@@ -227,7 +234,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
             const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
-                                 : *(const bf16x8*)(X + (size_t)xrow * K + k);
+                                 : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
         }
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sb0 + j) * kQ6KPacked;
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ6KPacked;
         qa[j][n] = ldg16(bp + hh * 64 + 16 * p);
         qb[j][n] = ldg16(bp + hh * 64 + 32 + 16 * p);
         qh[j][n] = ldg16(bp + 128 + hh * 32 + 16 * p);
@@ -248,7 +255,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K, K);
+      gemv_stage_x(smem, X, M, K, ldx);
       __syncthreads();
     }
 #pragma unroll
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
             const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
-                                 : *(const bf16x8*)(X + (size_t)xrow * K + k);
+                                 : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
         }
@@ -294,7 +301,7 @@ struct QPlan {
   int MT, NT, SBW, waves, tiles;
 };
 
-static QPlan qplan(int M, int N, int K, int epi) {
+static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
   QPlan p{};
   p.MT = (M + 15) / 16;
   p.NT = (epi == MS_GEMV_EPI_SWIGLU) ? 2 : 1;
@@ -325,9 +332,9 @@ bool qgemv_supported(int M, int N, int K, int epi) {
 
 template <int MT, int NT, int EPI>
 static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
-                     const QPlan& p, const GemvArgs& ga, hipStream_t s) {
+                     const QPlan& p, const GemvArgs& ga, hipStream_t s, int S = 1) {
   const size_t lds = qlds(p, M, K);
-  const dim3 grid(p.tiles), blk(64 * p.waves);
+  const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;
   } else {
@@ -367,6 +374,28 @@ void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K
     case 2: qgemv_go_mt<2>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
     case 3: qgemv_go_mt<3>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
     default: qgemv_go_mt<4>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
+  }
+}
+
+bool qgemv_split_supported(int M, int N, int K, int S) {
+  if (S < 1 || K % (256 * S)) return false;
+  return qgemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32);
+}
+
+// fp32 partial slabs [S][M][N] over S equal K ranges (super-block aligned); the caller
+// folds them (residual_rmsnorm_kernel / the decode attention prologue)
+void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
+                        hipStream_t s) {
+  if (M <= 0) return;
+  const int Ks = K / S;
+  const QPlan p = qplan(M, N, Ks, MS_GEMV_EPI_STORE_F32);
+  if (p.waves == 0) return;  // callers check qgemv_split_supported()
+  const GemvArgs ga{};
+  switch (p.MT) {
+    case 1: qgemv_go<1, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    case 2: qgemv_go<2, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    case 3: qgemv_go<3, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    default: qgemv_go<4, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
   }
 }
 

@@ -109,6 +109,9 @@ void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t*
 void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t seed, float scale,
                           hipStream_t s);
 bool qgemv_supported(int M, int N, int K, int epi);
+bool qgemv_split_supported(int M, int N, int K, int S);
+void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
+                        hipStream_t s);
 void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga, hipStream_t s);
 

@@ -25,7 +25,7 @@ K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC = range(6)
 
 EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
-    "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv",
+    "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv", "ms_op_qgemv_split",
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
@@ -83,6 +83,7 @@ def load() -> C.CDLL:
         "ms_op_dequant": (i32, [i32, vp, i64, vp, vp]),
         "ms_op_quant_rows": (i32, [i32, vp, i32, i32, vp, vp, vp]),
         "ms_op_qgemv": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, vp]),
+        "ms_op_qgemv_split": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, vp]),
         "ms_submit": (i32, [vp, pi32, i32, i32, u32, u64]),
         "ms_step": (i32, [vp]),
         "ms_poll": (i32, [vp, C.POINTER(MsResult), i32]),

@@ -442,6 +442,29 @@ def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
     assert rel(out.double().cpu(), exp.cpu()) < tol
 
 
+@pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
+@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("N,K,S", [(256, 3072, 6), (512, 3072, 4), (128, 8192, 4), (256, 8192, 2),
+                                   (64, 768, 3)])
+def test_qgemv_split_slabs_vs_fp64(lib, dev, qtype, M, N, K, S):
+    """Quantised split-K: slab s is the dequantised partial product over its K range (fp32
+    sum order only); the slabs add up to the full product; bad splits are refused."""
+    _, wbf, pk = _packed(lib, dev, qtype, N, K, 11 + M + S)
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + S)
+    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    slabs = torch.full((S, M, N), float("nan"), device=dev)
+    L.check(lib.ms_op_qgemv_split(X.data_ptr(), qtype, pk.data_ptr(), slabs.data_ptr(), M, N, K, S,
+                                  _stream()))
+    torch.cuda.synchronize()
+    Xd, Wd, ks = X.double().cpu(), wbf.double().cpu(), K // S
+    for s_ in range(S):
+        exp = Xd[:, s_ * ks:(s_ + 1) * ks] @ Wd[:, s_ * ks:(s_ + 1) * ks].T
+        assert rel(slabs[s_].double().cpu(), exp) < 2e-6, s_
+    assert rel(slabs.double().sum(0).cpu(), Xd @ Wd.T) < 2e-6
+    assert lib.ms_op_qgemv_split(X.data_ptr(), qtype, pk.data_ptr(), slabs.data_ptr(), M, N, K, 5,
+                                 _stream()) != 0
+
+
 def _quant_model(seed):
     """Tiny Q4_K_M-style model: raw blocks per matrix + the oracle's view of it
     (weights = bf16_rne(dequant(blocks)))."""
