@@ -488,17 +488,42 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
                                                                   bf16_t* __restrict__ out, int Hq,
                                                                   int nsplit) {
+  // every (m_s, l_s) pair is loaded at once (wave 0, two splits per lane) and the O loads
+  // are issued 8 at a time: the old serial split loop was a chain of dependent L2 round
+  // trips.  Sums keep the split order, so results are unchanged.
+  __shared__ float fw[128], lw[128];
   const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
   const float* p = ws + ((size_t)b * Hq + hq) * nsplit * 132;
-  float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, p[s * 132]);
+  if (d < 64) {
+    const float m0 = d < nsplit ? p[d * 132] : -INFINITY;
+    const float m1 = d + 64 < nsplit ? p[(d + 64) * 132] : -INFINITY;
+    const float l0 = d < nsplit ? p[d * 132 + 1] : 0.f;
+    const float l1 = d + 64 < nsplit ? p[(d + 64) * 132 + 1] : 0.f;
+    float M = fmaxf(m0, m1);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) M = fmaxf(M, __shfl_xor(M, o));
+    fw[d] = m0 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m0 - M);
+    fw[d + 64] = m1 == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m1 - M);
+    lw[d] = l0;
+    lw[d + 64] = l1;
+  }
+  __syncthreads();
   float L = 0.f, O = 0.f;
-  for (int s = 0; s < nsplit; ++s) {
-    const float ms_ = p[s * 132];
-    if (ms_ == -INFINITY) continue;
-    const float f = __builtin_amdgcn_exp2f(ms_ - M);
-    L += f * p[s * 132 + 1];
-    O += f * p[s * 132 + 2 + d];
+  const float* po = p + 2 + d;
+  int s = 0;
+  for (; s + 8 <= nsplit; s += 8) {
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = po[(s + q) * 132];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      L += fw[s + q] * lw[s + q];
+      O += fw[s + q] * v[q];
+    }
+  }
+  for (; s < nsplit; ++s) {
+    L += fw[s] * lw[s];
+    O += fw[s] * po[s * 132];
   }
   out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2bf(O / L);
 }
