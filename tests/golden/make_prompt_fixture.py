@@ -17,7 +17,10 @@ SRC = {"mapreduce": ("run_summarization_ollama_mapreduce.py", "Vui lòng viết 
        "mapreduce_critique": ("run_summarization_ollama_mapreduce_critique.py", "Văn bản:\n<content>"),
        "mapreduce_hierarchical": ("run_summarization_ollama_mapreduce_hierarchical.py", "<content>\n{content}\n\n</content>"),
        # the reduce prompt of the map-reduce graph (mapreduce.py:88-94), for mapsum/mapreduce.py
-       "reduce_mapreduce": ("run_summarization_ollama_mapreduce.py", "Sau đây là một tập hợp các bản tóm tắt:\n{docs}")}
+       "reduce_mapreduce": ("run_summarization_ollama_mapreduce.py", "Sau đây là một tập hợp các bản tóm tắt:\n{docs}"),
+       # mapsum/hierarchical.py: reduce (:104-112) and review (:297-311) prompts
+       "reduce_hierarchical": ("run_summarization_ollama_mapreduce_hierarchical.py", "Sau đây là một tập hợp các bản tóm tắt:\n<docs>"),
+       "review_hierarchical": ("run_summarization_ollama_mapreduce_hierarchical.py", "Bạn là một biên tập viên chuyên nghiệp")}
 
 
 def main():
