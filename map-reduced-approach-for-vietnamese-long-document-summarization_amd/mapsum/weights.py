@@ -5,8 +5,8 @@ Sources:
     bf16 values) -- used by the parity tests;
   * a Hugging Face Llama-3.2 checkpoint directory (``*.safetensors``; rotate-half RoPE
     convention, which is what the kernels implement) -- the real-weight path.  The
-    reference pulls ``llama3.2:3b`` through Ollama (README.md:28-33); a GGUF reader
-    (Q/K un-permutation + Q4_K/Q6_K dequant) is SURVEY.md §8d config 5, not yet built.
+    reference pulls ``llama3.2:3b`` through Ollama (README.md:28-33); its GGUF blobs load
+    through ``mapsum.gguf.load_gguf`` (Q/K un-permutation, float or Q4_K/Q6_K matrices).
 The engine itself fuses Q|K|V and interleaves gate/up rows on upload (csrc/engine.cpp
 ``ms_load_weight``), so callers always pass nn.Linear [out][in] tensors.
 """
