@@ -144,8 +144,8 @@ def pmc_traffic(weights):
     hits = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                          "profiles", "r*", f"pmc_traffic_{weights}.json")))
     if not hits:
-        return None
-    return json.load(open(hits[-1]))["traffic_bytes_per_launch"]
+        return None, None
+    return json.load(open(hits[-1]))["traffic_bytes_per_launch"], os.path.relpath(hits[-1], os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
@@ -236,8 +236,9 @@ def main():
             per_step = qgemv_bytes_per_step(cfg, B) if quant else gemv_bytes_per_step(cfg, B)
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
+            traffic, traffic_src = pmc_traffic(args.weights)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(args.weights),
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
                               + " decode QKV/O/gate-up/down projections)",
                     "bytes_per_launch": int(bytes_total / launches),
