@@ -79,6 +79,13 @@ def qgemv_bytes_per_step(cfg, B):
     return tot
 
 
+def lm_head_bytes_per_step(cfg, B, quant=False):
+    """The decode lm_head launch: the (tied) vocab matrix once -- Q6_K repacked to 224 B per
+    256 weights under Q4_K_M (csrc/engine.cpp q4_k_m_type) -- plus B rows in, fp32 logits out."""
+    w = cfg.vocab * cfg.hidden * (224 / 256 if quant else 2)
+    return w + 2 * B * cfg.hidden + 4 * B * cfg.vocab
+
+
 def prefill_flops_per_chunk(cfg, P):
     """2*params_linear*P + lm_head on the last token + causal attention."""
     H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
@@ -226,21 +233,22 @@ def main():
         # runs after the timed region because an event pair per launch (112 per decode
         # step) costs ~0.6 ms/step and would distort `value`.
         eng.reset_stats()
-        eng.set_profiling(1 << L.K_GEMV)
+        eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD))
         one_step()
         eng.set_profiling(0)
         sp = eng.stats()
-        launches = sp["kernel_launches"][L.K_GEMV]
+        launches = sp["kernel_launches"][L.K_GEMV] + sp["kernel_launches"][L.K_LMHEAD]
         if launches:
-            gemv_s = sp["kernel_ms"][L.K_GEMV] / 1e3
-            per_step = qgemv_bytes_per_step(cfg, B) if quant else gemv_bytes_per_step(cfg, B)
+            gemv_s = (sp["kernel_ms"][L.K_GEMV] + sp["kernel_ms"][L.K_LMHEAD]) / 1e3
+            per_step = (qgemv_bytes_per_step(cfg, B) if quant else gemv_bytes_per_step(cfg, B)) \
+                + lm_head_bytes_per_step(cfg, B, quant)
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
             traffic, traffic_src = pmc_traffic(args.weights)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
-                              + " decode QKV/O/gate-up/down projections)",
+                              + " decode weight stream: QKV/O/gate-up/down projections + lm_head)",
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
                     "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}

@@ -18,6 +18,8 @@
 // per wave-step), dequantises in registers to exactly the bf16 values of the bf16 copy,
 // and feeds v_mfma_f32_16x16x32_bf16 -- decode with Q4_K_M weights therefore computes
 // the same model as prefill, only from 3.6x fewer weight bytes.
+#include <cstdlib>
+
 #include "gemv_common.h"
 
 namespace ms {
@@ -308,6 +310,8 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
   p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
   const int nsb = K / 256;
   p.SBW = nsb > 16 ? 2 : 1;
+  static const int env_sbw = [] { const char* v = getenv("MS_QSBW"); return v ? atoi(v) : 0; }();
+  if ((env_sbw == 1 || env_sbw == 2) && nsb % env_sbw == 0 && nsb / env_sbw <= 16) p.SBW = env_sbw;  // tuning hook
   p.waves = (nsb % p.SBW == 0) ? nsb / p.SBW : 0;
   if (p.waves > 16) p.waves = 0;
   return p;
