@@ -1,21 +1,24 @@
 """bench.py -- map-phase chunks/s of the MI355X engine (BASELINE.json metric).
 
-A "step" = one map phase over one batch: every GPU takes its chunks_per_gpu synthetic
-2048-token chunks (the workload of BASELINE.json configs[1]: one 16k-token doc split
-into 8 chunks), prefills them packed, decodes exactly 256 greedy tokens each
-(ignore_eos), and the per-chunk summary ids are gathered to rank 0
-over RCCL.  value = chunks of all ranks / max-over-ranks wall time.  N > 1 is weak
-scaling: each rank owns its own document's chunks.
+A "step" = one map phase over one batch of synthetic chunks.  Default (BASELINE.json
+configs[1]): every GPU takes 8 synthetic 2048-token chunks (one 16k-token doc split in
+8), prefills them packed, decodes exactly 256 greedy tokens each (ignore_eos, SURVEY.md
+§8d), and the per-chunk summary ids are gathered to rank 0 over RCCL.  ``--docs D``
+(configs[2]): D docs x 8 chunks, sharded over the ranks (chunk i -> rank i mod N), run
+as one continuous batch of at most ``--max-batch`` sequences per GPU.  value = chunks of
+all ranks / max-over-ranks wall time.  N > 1 is weak scaling in the default mode (each
+rank owns its own document: SURVEY.md §8e).
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W]      # N > 1: launches N ranks itself
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -29,17 +32,19 @@ import numpy as np  # noqa: E402
 
 METRIC = "map-phase chunks/sec (2k-tok chunk, 256-tok summary) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
-BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA
+BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+CHUNKS_PER_DOC = 8          # BASELINE.json configs[0..2]: a 16k-token doc in 2k chunks
 
 
-def synthetic_chunks(n, prompt_len, doc, vocab, bos, seed=0):
+def synthetic_chunks(n, prompt_len, doc, vocab, bos, seed=0, first_chunk=0):
     """Token ids of n chunks: BOS + Llama-3 header ids + uniform body over [0, 128000)
-    (no tokenizer / dataset offline; timing of dense ops does not depend on values)."""
+    (no tokenizer / dataset offline; timing of dense ops does not depend on values).
+    Chunk c of doc d is the same wherever it runs (seeded by (d, c))."""
     head = [bos, 128006, 9125, 128007, 271, 128009, 128006, 882, 128007, 271]
-    rng = np.random.default_rng(seed + 1000 * doc)
     tail = [128009, 128006, 78191, 128007, 271]
     out = []
-    for _ in range(n):
+    for c in range(first_chunk, first_chunk + n):
+        rng = np.random.default_rng((seed, doc, c))
         body = rng.integers(0, min(128000, vocab), size=prompt_len - len(head) - len(tail))
         ids = np.array(head + body.tolist() + tail, np.int32)
         out.append(np.clip(ids, 0, vocab - 1))
@@ -86,6 +91,14 @@ def lm_head_bytes_per_step(cfg, B, quant=False):
     return w + 2 * B * cfg.hidden + 4 * B * cfg.vocab
 
 
+def decode_weight_bytes(cfg, quant=False):
+    """Weight bytes one decode step streams (every layer matrix + the lm_head): SURVEY.md
+    §8d's W = 6,425,149,440 B for bf16 Llama-3.2-3B."""
+    if not quant:
+        return cfg.weight_bytes
+    return qgemv_bytes_per_step(cfg, 0) + cfg.vocab * cfg.hidden * 224 / 256
+
+
 def prefill_flops_per_chunk(cfg, P):
     """2*params_linear*P + lm_head on the last token + causal attention."""
     H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
@@ -94,73 +107,61 @@ def prefill_flops_per_chunk(cfg, P):
     return 2 * lin * P + 2 * cfg.vocab * H + attn
 
 
-def cpu_baseline(cfg, prompt_len, gen_len, decode_sample=16):
-    """Oracle (numpy, CPU) on a bounded sample of the same workload, scaled to one chunk:
-    one full-width layer prefilled over a prompt_len chunk + decode_sample cached decode
-    steps through that layer + the tied lm_head, times n_layers / gen_len."""
-    from oracle.llama_ref import OracleLlama
-    one = cfg.with_(n_layers=1)
-    rng = np.random.default_rng(0)
-    H, D = cfg.hidden, cfg.head_dim
-
-    def lin(r, c):
-        return (rng.standard_normal((r, c), dtype=np.float32) * 0.02)
-
-    w = {"embed": lin(cfg.vocab, H), "final_norm": np.ones(H, np.float32),
-         "layers": [{"attn_norm": np.ones(H, np.float32), "ffn_norm": np.ones(H, np.float32),
-                     "wq": lin(cfg.n_heads * D, H), "wk": lin(cfg.n_kv_heads * D, H),
-                     "wv": lin(cfg.n_kv_heads * D, H), "wo": lin(H, cfg.n_heads * D),
-                     "w_gate": lin(cfg.ffn, H), "w_up": lin(cfg.ffn, H), "w_down": lin(H, cfg.ffn)}]}
-    w["lm_head"] = w["embed"]
-    o = OracleLlama(one, w)
-    ids = rng.integers(0, 128000, size=prompt_len)
-    cache = o.new_cache()
-    t0 = time.perf_counter()
-    logits, _ = o.forward(ids, cache)
-    t_pre = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    for _ in range(decode_sample):
-        logits, _ = o.forward([int(np.argmax(logits))], cache)
-    t_dec = (time.perf_counter() - t0) / decode_sample
-    # lm_head is paid once per token, the layer n_layers times
-    t0 = time.perf_counter()
-    for _ in range(4):
-        _ = w["embed"] @ np.ones(H, np.float32)
-    t_head = (time.perf_counter() - t0) / 4
-    t_layer_dec = max(t_dec - t_head, 1e-9)
-    t_layer_pre = max(t_pre - t_head, 1e-9)
-    chunk_s = cfg.n_layers * t_layer_pre + t_head + (gen_len - 1) * (cfg.n_layers * t_layer_dec + t_head)
-    try:
-        import threadpoolctl
-        cores = max(p["num_threads"] for p in threadpoolctl.threadpool_info()) if threadpoolctl.threadpool_info() else 1
-    except Exception:
-        cores = os.cpu_count() or 1
-    return {"value": 1.0 / chunk_s, "unit": "chunks/s", "cores": int(cores), "kind": "port",
-            "sample": (f"numpy oracle, Llama-3.2-3B width, 1 of {cfg.n_layers} layers: {prompt_len}-tok "
-                       f"prefill ({t_pre:.2f}s) + {decode_sample} cached decode steps "
-                       f"({t_dec * 1e3:.1f} ms/step incl. lm_head {t_head * 1e3:.1f} ms), "
-                       f"scaled to {cfg.n_layers} layers x {gen_len} tokens")}
+def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=16):
+    """BASELINE.md §2 fallback (Ollama and the GGUF are absent on the box): the torch-CPU
+    bf16 restatement of the same map call (oracle/torch_cpu.py), all 28 layers, on one
+    chunk of this workload: its full 2048-token prefill + ``decode_sample`` greedy decode
+    steps, extrapolated to the 256 generated tokens."""
+    import torch
+    from oracle.torch_cpu import time_chunk
+    r = time_chunk(cfg, prompt_ids, gen_len, decode_sample=decode_sample)
+    return {"value": round(1.0 / r["chunk_s"], 5), "unit": "chunks/s", "cores": int(r["threads"]),
+            "kind": "port",
+            "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16, "
+                       f"{cfg.n_layers}-layer Llama-3.2-3B, 1 chunk: {len(prompt_ids)}-tok prefill "
+                       f"{r['prefill_s']:.2f} s + {r['decode_steps_timed']} decode steps at "
+                       f"{r['decode_step_s'] * 1e3:.1f} ms, extrapolated to {gen_len} tokens "
+                       f"({r['chunk_s']:.1f} s/chunk)")}
 
 
-def pmc_traffic(weights):
+def pmc_traffic(weights, B, prompt_len):
     """HBM bytes per GEMV launch from the committed rocprofv3 --pmc passes of this same
     workload (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic_from_pmc.py, run by
-    tools/gpu_round.sh); None when no such measurement is committed.  PMC counters cannot
-    be read from inside a timed run, so this is the profiler's number, not a live one."""
+    tools/gpu_round.sh), or (None, None) when none was taken at this B and prompt length.
+    PMC counters cannot be read inside a timed run: this is the profiler's number."""
     import glob
-    hits = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                         "profiles", "r*", f"pmc_traffic_{weights}.json")))
-    if not hits:
-        return None, None
-    return json.load(open(hits[-1]))["traffic_bytes_per_launch"], os.path.relpath(hits[-1], os.path.dirname(os.path.abspath(__file__)))
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{weights}.json")))
+    for h in reversed(hits):
+        d = json.load(open(h))
+        wl = d.get("workload", {})
+        if wl.get("chunks_per_gpu") == B and wl.get("prompt_len") == prompt_len:
+            return d["traffic_bytes_per_launch"], os.path.relpath(h, ROOT)
+    return None, None
 
 
-def main():
+def _spawn_ranks(n):
+    """`python bench.py --gpus N` outside torchrun: start N ranks (one per GPU) as
+    children through torch.distributed.run, before this process touches any GPU, and
+    exit with their status."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--chunks-per-gpu", type=int, default=8)
+    ap.add_argument("--docs", type=int, default=0,
+                    help="configs[2]: D docs x 8 chunks over all ranks as one continuous batch per GPU")
+    ap.add_argument("--max-batch", type=int, default=64,
+                    help="--docs mode: sequences in flight per GPU (continuous batching)")
     ap.add_argument("--prompt-len", type=int, default=2048)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--model", default="llama3.2-3b")
@@ -168,14 +169,31 @@ def main():
                     help="q4_k_m = BASELINE configs[4]: random Q4_K/Q6_K blocks, K-quant decode GEMVs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip HIP-event timing of the GEMV class")
-    args = ap.parse_args()
+    ap.add_argument("--no-check", action="store_true", help="skip the output self-checks")
+    return ap.parse_args(argv)
+
+
+def local_units(args, rank, world):
+    """(doc, chunk) units of this rank.  Default: the rank's own doc; --docs: the global
+    (doc, chunk) list sharded statically (uniform chunks)."""
+    from mapsum.dist import Unit, shard_static
+    if args.docs:
+        units = [Unit(d, c, args.prompt_len) for d in range(args.docs) for c in range(CHUNKS_PER_DOC)]
+        return shard_static(units, rank, world)
+    return [Unit(rank, i, args.prompt_len) for i in range(args.chunks_per_gpu)]
+
+
+def main():
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
 
     from mapsum import _lib as L
     from mapsum.config import CONFIGS
-    from mapsum.dist import Unit, env_rank, gather_summaries, pack_results
+    from mapsum.dist import env_rank, gather_summaries, pack_results
     from mapsum.engine import Engine
 
     cfg = CONFIGS[args.model]
@@ -185,22 +203,29 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-    B = args.chunks_per_gpu
+    units = local_units(args, rank, world)
+    n_local = len(units)
+    max_rows = max(len(local_units(args, r, world)) for r in range(world))
+    B = min(args.max_batch, n_local) if args.docs else n_local
     max_ctx = args.prompt_len + args.gen_len
     eng = Engine(cfg, device=local_rank, max_batch=B, max_ctx=max_ctx,
-                 max_prefill_tokens=B * args.prompt_len)
+                 max_prefill_tokens=min(B, 8) * args.prompt_len)
     quant = args.weights == "q4_k_m"
     if quant:
         eng.init_synthetic_q(seed=2, scale=0.02, norm_jitter=0.0)
     else:
         eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
-    chunks = synthetic_chunks(B, args.prompt_len, doc=rank, vocab=cfg.vocab, bos=cfg.bos_id)
-    units = [Unit(rank, i, args.prompt_len) for i in range(B)]
+    chunks = [synthetic_chunks(1, args.prompt_len, u.doc, cfg.vocab, cfg.bos_id, first_chunk=u.chunk)[0]
+              for u in units]
+    gather_s = [0.0]
 
     def one_step():
         res = eng.generate(chunks, num_predict=args.gen_len, ignore_eos=True)
         packed = pack_results(units, [r.ids for r in res], args.gen_len)
-        return gather_summaries(packed, B, device=dev)
+        t0 = time.perf_counter()
+        rows = gather_summaries(packed, max_rows, device=dev)
+        gather_s[0] += time.perf_counter() - t0
+        return res, rows
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -211,10 +236,13 @@ def main():
     for _ in range(args.warmup):
         one_step()
     eng.reset_stats()
+    gather_s[0] = 0.0
+    outs = []
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        rows = one_step()
+        res, rows = one_step()
+        outs.append([r.ids for r in res])
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
@@ -222,29 +250,41 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     st = eng.stats()
-    total_chunks = world * B * args.steps
+    total_chunks = sum(len(local_units(args, r, world)) for r in range(world)) * args.steps
     value = total_chunks / dt
-    assert rows is not None and len(rows) == world * B
+    assert rows is not None and int((rows[:, 2] >= 0).sum()) == total_chunks // args.steps
+
+    # self-checks (outside the timed region): every step produced the same summaries, each
+    # of the full length, and a chunk's summary does not depend on its batch companions
+    check = None
+    if not args.no_check:
+        same = all(o == outs[0] for o in outs[1:])
+        full = all(len(ids) == args.gen_len for ids in outs[0])
+        alone = eng.generate([chunks[0]], num_predict=args.gen_len, ignore_eos=True)[0].ids
+        check = {"deterministic_across_steps": same, "full_length": full,
+                 "batch_invariant_chunk0": alone == outs[0][0]}
+        assert same and full and check["batch_invariant_chunk0"], check
 
     roof = None
     if not args.no_roofline:
-        # Roofline of the dominant kernel class (the decode projections): one more map
-        # step with HIP events bracketing every gemv launch on the engine's stream.  It
-        # runs after the timed region because an event pair per launch (112 per decode
+        # Roofline of the dominant kernel class (the decode weight stream): one more map
+        # step with HIP events bracketing every GEMV launch on the engine's stream.  It
+        # runs after the timed region because an event pair per launch (113 per decode
         # step) costs ~0.6 ms/step and would distort `value`.
         eng.reset_stats()
         eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD))
-        one_step()
+        eng.generate(chunks[:min(len(chunks), B)], num_predict=min(args.gen_len, 64), ignore_eos=True)
         eng.set_profiling(0)
         sp = eng.stats()
         launches = sp["kernel_launches"][L.K_GEMV] + sp["kernel_launches"][L.K_LMHEAD]
         if launches:
             gemv_s = (sp["kernel_ms"][L.K_GEMV] + sp["kernel_ms"][L.K_LMHEAD]) / 1e3
-            per_step = (qgemv_bytes_per_step(cfg, B) if quant else gemv_bytes_per_step(cfg, B)) \
-                + lm_head_bytes_per_step(cfg, B, quant)
+            bstep = sp["decode_tokens"] / max(sp["decode_steps"], 1)
+            per_step = (qgemv_bytes_per_step(cfg, bstep) if quant else gemv_bytes_per_step(cfg, bstep)) \
+                + lm_head_bytes_per_step(cfg, bstep, quant)
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
-            traffic, traffic_src = pmc_traffic(args.weights)
+            traffic, traffic_src = pmc_traffic(args.weights, B, args.prompt_len)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                     "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
@@ -252,30 +292,53 @@ def main():
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
                     "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}
-    pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * B * args.steps
+    # whole-phase rooflines from the timed run's own event-timed prefill / decode passes
+    pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * n_local * args.steps
+    pre_tf = pre_flops / (st["prefill_ms"] / 1e3) / 1e12 if st["prefill_ms"] else None
+    kvb = cfg.kv_bytes_per_token
+    dec_bytes = (st["decode_steps"] * decode_weight_bytes(cfg, quant) + st["decode_kv_tokens"] * kvb
+                 + st["decode_tokens"] * kvb)
+    dec_gbs = dec_bytes / (st["decode_ms"] / 1e3) / 1e9 if st["decode_ms"] else None
+    roof_pre = {"bound": "mfma", "achieved": round(pre_tf, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(pre_tf / BF16_PEAK_TFLOPS, 4),
+                "flops_per_chunk": prefill_flops_per_chunk(cfg, args.prompt_len),
+                "method": "SURVEY.md §8d prefill FLOP / event-timed prefill passes (all kernels)"} if pre_tf else None
+    roof_dec = {"bound": "hbm", "achieved": round(dec_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(dec_gbs / HBM_PEAK_GBS, 4),
+                "bytes_per_step": round(dec_bytes / max(st["decode_steps"], 1)),
+                "method": "weights + KV reads + KV writes (SURVEY.md §8d) / event-timed decode steps "
+                          "(all kernels)"} if dec_gbs else None
     out = {
         "metric": METRIC, "value": round(value, 4), "unit": "chunks/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
         "data": ("synthetic (random Q4_K/Q6_K blocks in the Q4_K_M mix, seed 2, uniform token ids)"
                  if quant else "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)"),
-        "config": {"workload": f"{'configs[4]' if quant else 'configs[1]'}: {B} x {args.prompt_len}-tok chunks -> {args.gen_len}-tok "
-                               f"greedy summaries per GPU (ignore_eos), batched prefill + decode, "
-                               f"summary ids gathered to rank 0",
-                   "model": cfg.name, "weights": args.weights, "chunks_per_gpu": B, "prompt_tokens": args.prompt_len,
-                   "summary_tokens": args.gen_len, "global_batch": world * B,
+        "config": {"workload": (f"configs[2]: {args.docs} docs x {CHUNKS_PER_DOC} x {args.prompt_len}-tok "
+                                f"chunks over {world} GPU(s) ({n_local} per GPU, <= {B} in flight, "
+                                f"continuous batching)" if args.docs else
+                                f"{'configs[4]' if quant else 'configs[1]'}: {B} x {args.prompt_len}-tok chunks")
+                               + f" -> {args.gen_len}-tok greedy summaries (ignore_eos), batched prefill + "
+                                 f"decode, summary ids gathered to rank 0",
+                   "model": cfg.name, "weights": args.weights, "chunks_per_gpu": n_local, "max_batch": B,
+                   "prompt_tokens": args.prompt_len, "summary_tokens": args.gen_len,
+                   "global_batch": total_chunks // args.steps,
                    "seq_len": args.prompt_len + args.gen_len, "parallelism": f"chunk-dp{world}"},
         "breakdown": {"prefill_ms_per_step": round(st["prefill_ms"] / args.steps, 2),
                       "decode_ms_per_step": round(st["decode_ms"] / args.steps, 2),
                       "decode_steps": st["decode_steps"],
-                      "prefill_tflops": round(pre_flops / (st["prefill_ms"] / 1e3) / 1e12, 1)
-                      if st["prefill_ms"] else None,
-                      "gemv_ms_total": round(st["kernel_ms"][L.K_GEMV], 2)},
+                      "decode_ms_per_decode_step": round(st["decode_ms"] / max(st["decode_steps"], 1), 4),
+                      "gather_ms_per_step": round(gather_s[0] / args.steps * 1e3, 3),
+                      "prefill_tflops": round(pre_tf, 1) if pre_tf else None},
         "roofline": roof,
+        "roofline_prefill": roof_pre,
+        "roofline_decode": roof_dec,
+        "check": check,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, args.prompt_len, args.gen_len)
+        eng.close()
+        out["cpu_baseline"] = cpu_baseline(cfg, chunks[0], args.gen_len)
     eng.close()
     if rank == 0:
         print(json.dumps(out), flush=True)

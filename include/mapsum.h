@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 1
+#define MS_ABI_VERSION 2
 
 /* status codes */
 #define MS_OK 0
@@ -48,7 +48,10 @@ extern "C" {
 /* finish reasons (ms_result.finish_reason) -- Ollama's done_reason "stop"/"length" */
 #define MS_FINISH_EOS 1
 #define MS_FINISH_LENGTH 2
-#define MS_FINISH_ERROR 3
+#define MS_FINISH_ERROR 3 /* this chunk only: no finite logit (NaN/Inf in its activations);
+                             the other chunks of the batch are unaffected.  The reference has
+                             no retry (run_full_evaluation_pipeline.py:627-638 marks the whole
+                             model failed); the Python host re-queues such a chunk once. */
 
 /* ms_submit flags */
 #define MS_FLAG_IGNORE_EOS 1u /* bench mode: always generate num_predict tokens */
@@ -81,7 +84,7 @@ typedef struct ms_config {
   int32_t tie_embeddings;
   /* engine */
   int32_t device;               /* HIP device ordinal                         */
-  int32_t max_batch;            /* sequences in flight (<= 256)               */
+  int32_t max_batch;            /* sequences in flight (<= 1024)              */
   int32_t max_ctx;              /* prompt + generated tokens per sequence     */
   int32_t max_prefill_tokens;   /* packed prompt tokens per prefill pass      */
   int32_t n_pages;              /* KV pages of 64 tokens; 0 = enough for all  */
@@ -108,6 +111,8 @@ typedef struct ms_stats {
                                    0 gemm(prefill) 1 attn_prefill 2 gemv(decode)
                                    3 attn_decode 4 lm_head 5 norm/rope/misc     */
   int64_t kernel_launches[8];
+  int64_t decode_kv_tokens;     /* sum over decode steps and rows of the keys attended
+                                   (the KV-read term of SURVEY.md §8d's decode bytes)  */
 } ms_stats;
 
 typedef struct ms_engine ms_engine;

@@ -316,6 +316,13 @@ struct ms_engine {
     gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
   }
 
+  // Captured decode graphs bake in the weight form (bf16 vs K-quant stream) and the split
+  // choices: any weight (re)load invalidates them.
+  void drop_graphs() {
+    for (auto& kv : decode_graphs) (void)hipGraphExecDestroy(kv.second);
+    decode_graphs.clear();
+  }
+
   int32_t* upload_args(const std::vector<int32_t>& a) {
     REQUIRE(a.size() <= args_cap, MS_EINVAL, "step arguments exceed the staging buffer");
     std::memcpy(args_h, a.data(), a.size() * sizeof(int32_t));
@@ -385,7 +392,7 @@ void validate_config(const ms_config& c) {
   REQUIRE(c.hidden == c.n_heads * c.head_dim, MS_EINVAL, "hidden must equal n_heads*head_dim");
   REQUIRE(c.hidden % 256 == 0 && c.ffn % 256 == 0, MS_EINVAL, "hidden and ffn must be multiples of 256");
   REQUIRE(c.vocab % 16 == 0 && c.vocab > 0, MS_EINVAL, "vocab must be a multiple of 16");
-  REQUIRE(c.max_batch >= 1 && c.max_batch <= 256, MS_EINVAL, "max_batch must be in [1,256]");
+  REQUIRE(c.max_batch >= 1 && c.max_batch <= 1024, MS_EINVAL, "max_batch must be in [1,1024]");
   REQUIRE(c.max_ctx >= 64 && c.max_ctx <= 131072, MS_EINVAL, "max_ctx must be in [64,131072]");
   REQUIRE(c.max_prefill_tokens >= 1, MS_EINVAL, "max_prefill_tokens must be >= 1");
   REQUIRE(c.n_eos >= 0 && c.n_eos <= 8, MS_EINVAL, "n_eos must be in [0,8]");
@@ -562,6 +569,7 @@ static TensorDst tensor_dst(ms_engine& E, int tensor, int layer) {
 
 int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host, int64_t n) {
   if (!e) return MS_EINVAL;
+  e->drop_graphs();
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     REQUIRE(host != nullptr, MS_EINVAL, "null weight buffer");
@@ -622,6 +630,7 @@ static void load_quant(ms_engine& E, int tensor, int layer, int type, const uint
 int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t type, const void* host,
                      int64_t n_bytes) {
   if (!e) return MS_EINVAL;
+  e->drop_graphs();
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     REQUIRE(host != nullptr, MS_EINVAL, "null block buffer");
@@ -660,6 +669,7 @@ static int q4_k_m_type(int tensor, int layer, int n_layers) {
 
 int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float jitter) {
   if (!e) return MS_EINVAL;
+  e->drop_graphs();
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     HIP_OK(hipSetDevice(E.cfg.device));
@@ -701,6 +711,7 @@ int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float jitter) 
 
 int ms_init_synthetic(ms_engine* e, uint64_t seed, float std_, float jitter) {
   if (!e) return MS_EINVAL;
+  e->drop_graphs();
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     HIP_OK(hipSetDevice(E.cfg.device));
@@ -765,6 +776,10 @@ static bool is_eos(const ms_engine& E, int32_t t) {
 
 // returns true if the sequence finished with this token
 static bool accept_token(ms_engine& E, Seq& s, int32_t t) {
+  if (t < 0 || t >= E.V) {  // no finite logit (NaN/Inf in this chunk's activations)
+    s.finish = MS_FINISH_ERROR;
+    return true;
+  }
   if (!(s.flags & MS_FLAG_IGNORE_EOS) && is_eos(E, t)) {
     s.finish = MS_FINISH_EOS;
     return true;
@@ -866,7 +881,13 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   E.prof_begin(K_MISC);
   launch_rmsnorm(E.x, E.final_norm, E.xb, S, E.H, E.cfg.norm_eps, d + o_last, E.stream);
   E.prof_end(K_MISC);
-  E.gemm_or_gemv(E.xb, E.lm_head, E.logits, S, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
+  // the first token goes through the decode lm_head GEMV in row groups of <= 64: its sum
+  // order is then the decode steps' one whatever the number of admitted prompts
+  for (int r0 = 0; r0 < S; r0 += ms_engine::kMaxSlabRows) {
+    const int rows = std::min(S - r0, (int)ms_engine::kMaxSlabRows);
+    E.gemm_or_gemv(E.xb + (size_t)r0 * E.H, E.lm_head, E.logits + (size_t)r0 * E.V, rows, E.V, E.H, E.V,
+                   MS_EPI_STORE_F32, true, K_LMHEAD);
+  }
   E.prof_begin(K_MISC);
   launch_argmax(E.logits, S, E.V, E.ids_out_d, E.stream);
   E.prof_end(K_MISC);
@@ -990,6 +1011,7 @@ int ms_step(ms_engine* e) {
       E.stats.decode_steps += 1;
       E.stats.decode_tokens += (int64_t)sub.size();
       for (size_t i = 0; i < sub.size(); ++i) {
+        E.stats.decode_kv_tokens += sub[i]->len + 1;
         sub[i]->len += 1;
         accept_token(E, *sub[i], next[i]);
       }

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(1024) void argmax_kernel(const float* __restrict__ 
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 16; ++w) amax_merge(v, idx, sv[w], si[w]);
-    out[blockIdx.x] = idx == 0x7FFFFFFF ? 0 : idx;
+    // no finite maximum (a NaN/Inf row): -1 tells the engine this chunk failed
+    out[blockIdx.x] = (idx == 0x7FFFFFFF || !__builtin_isfinite(v)) ? -1 : idx;
   }
 }
 

@@ -12,7 +12,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmapsum.so")
 
-MS_ABI_VERSION = 1
+MS_ABI_VERSION = 2
 MS_OK, MS_EIO, MS_ENOMEM, MS_EBUSY, MS_EINVAL, MS_ENOSPC = 0, -5, -12, -16, -22, -28
 MS_FINISH_EOS, MS_FINISH_LENGTH, MS_FINISH_ERROR = 1, 2, 3
 MS_FLAG_IGNORE_EOS = 1
@@ -55,7 +55,8 @@ class MsStats(C.Structure):
     _fields_ = [("prefill_tokens", C.c_int64), ("decode_tokens", C.c_int64),
                 ("prefill_passes", C.c_int64), ("decode_steps", C.c_int64), ("finished", C.c_int64),
                 ("prefill_ms", C.c_double), ("decode_ms", C.c_double),
-                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8)]
+                ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8),
+                ("decode_kv_tokens", C.c_int64)]
 
 
 _lib = None

@@ -50,7 +50,7 @@ class MapBackend:
         self._queue = []          # (ids, num_predict, future) waiting for the driver
         self._inflight = {}       # tag -> future
         self._driver = None
-        self._tag = 1 << 40  # async tags live above the engine's own generate() tags
+        self._tag = _ASYNC_TAG0
 
     # -- text <-> ids ----------------------------------------------------------
     def encode_prompt(self, prompt: str) -> list:
@@ -58,7 +58,11 @@ class MapBackend:
 
     # -- synchronous path (one chunk, or a list of chunks) ----------------------
     def generate_ids(self, id_lists, num_predict: int) -> list:
-        return self._pool.submit(self.engine.generate, id_lists, num_predict).result()
+        res = self._pool.submit(self.engine.generate, id_lists, num_predict).result()
+        for r in res:
+            if r.finish == "error":  # failed twice (Engine.generate re-queues once)
+                raise RuntimeError("mapsum: chunk failed twice (no finite logit)")
+        return res
 
     def generate(self, prompts, num_predict: int) -> list:
         ids = [self.encode_prompt(p) for p in prompts]
@@ -67,6 +71,11 @@ class MapBackend:
 
     # -- asynchronous path: continuous batching across concurrent callers ---------
     async def agenerate(self, prompt: str, num_predict: int) -> str:
+        return (await self.agenerate_full(prompt, num_predict))[0]
+
+    async def agenerate_full(self, prompt: str, num_predict: int):
+        """(text, finish) with finish in {"eos", "length"} -- Ollama's done_reason
+        "stop" / "length"."""
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         ids = self.encode_prompt(prompt)
@@ -74,36 +83,61 @@ class MapBackend:
             self._tag += 1
             tag = self._tag
         self._queue.append((tag, ids, num_predict))
-        self._inflight[tag] = fut
+        self._inflight[tag] = (fut, ids, num_predict, 1)  # one re-queue left
         if self._driver is None or self._driver.done():
             self._driver = asyncio.ensure_future(self._drive())
         r = await fut
-        return self.tok.decode(r.ids)
+        return self.tok.decode(r.ids), r.finish
 
     def _tick(self, new):
+        """Engine thread: submit the new requests (a request the engine refuses fails
+        alone), run one scheduler iteration, return this backend's finished results."""
+        refused = []
         for tag, ids, n in new:
-            self.engine.submit(ids, n, tag=tag)
+            try:
+                self.engine.submit(ids, n, tag=tag)
+            except Exception as e:  # noqa: BLE001 -- e.g. ENOSPC: prompt + num_predict > max_ctx
+                refused.append((tag, e))
         self.engine.step()
-        return self.engine.poll()
+        self.engine.collect()
+        return refused, self.engine.take_where(lambda t: t > _ASYNC_TAG0)
 
     async def _drive(self):
         loop = asyncio.get_running_loop()
         try:
             while self._queue or self._inflight:
                 new, self._queue = self._queue, []
-                done = await loop.run_in_executor(self._pool, self._tick, new)
-                for r in done:
-                    fut = self._inflight.pop(r.tag, None)
+                refused, done = await loop.run_in_executor(self._pool, self._tick, new)
+                for tag, e in refused:
+                    fut = self._inflight.pop(tag, (None,))[0]
                     if fut is not None and not fut.done():
+                        fut.set_exception(RuntimeError(f"mapsum: request refused: {e}"))
+                for r in done:
+                    ent = self._inflight.pop(r.tag, None)
+                    if ent is None:
+                        continue
+                    fut, ids, n, retries = ent
+                    if fut.done():
+                        continue
+                    if r.finish != "error":
                         fut.set_result(r)
-        except Exception as e:  # fail every waiter loudly (raise_for_status semantics)
-            for fut in self._inflight.values():
-                if not fut.done():
-                    fut.set_exception(RuntimeError(f"mapsum engine failed: {e}"))
+                    elif retries > 0:  # SURVEY.md §5: a failed chunk is re-queued once
+                        with self._lock:
+                            self._tag += 1
+                            tag = self._tag
+                        self._queue.append((tag, ids, n))
+                        self._inflight[tag] = (fut, ids, n, retries - 1)
+                    else:
+                        fut.set_exception(RuntimeError("mapsum: chunk failed twice (no finite logit)"))
+        except Exception as e:  # the engine itself failed: every waiter fails loudly
+            for ent in self._inflight.values():
+                if not ent[0].done():
+                    ent[0].set_exception(RuntimeError(f"mapsum engine failed: {e}"))
             self._inflight.clear()
             raise
 
 
+_ASYNC_TAG0 = 1 << 40  # async tags live above the engine's own generate() tags
 _BACKENDS: dict = {}
 _FACTORY = None
 

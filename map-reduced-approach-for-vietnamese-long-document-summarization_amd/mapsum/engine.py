@@ -29,7 +29,66 @@ class Result:
 _FINISH = {L.MS_FINISH_EOS: "eos", L.MS_FINISH_LENGTH: "length", L.MS_FINISH_ERROR: "error"}
 
 
-class Engine:
+class RequestQueue:
+    """The request-level half of an engine, over four primitives the subclass provides:
+    ``submit(ids, n, ignore_eos, tag) -> tag``, ``step() -> pending``, ``poll() -> [Result]``.
+
+    Finished results are parked in a mailbox keyed by tag, so several submitters (the
+    synchronous generate() and MapBackend's async driver) can share one engine: each
+    takes only its own tags and never consumes -- or counts -- another caller's."""
+
+    _mailbox: dict
+
+    def collect(self) -> None:
+        """Move every finished result into the mailbox."""
+        while True:
+            got = self.poll()
+            for r in got:
+                self._mailbox[r.tag] = r
+            if len(got) < 256:
+                return
+
+    def take(self, tags) -> dict:
+        """Remove and return the mailbox entries of ``tags`` that have finished."""
+        return {t: self._mailbox.pop(t) for t in list(tags) if t in self._mailbox}
+
+    def take_where(self, pred) -> list:
+        """Remove and return the mailbox entries whose tag satisfies ``pred``."""
+        mine = [t for t in self._mailbox if pred(t)]
+        return [self._mailbox.pop(t) for t in mine]
+
+    def generate(self, prompts, num_predict: int, ignore_eos: bool = False, retries: int = 1) -> list:
+        """Run every prompt (list of id lists) to completion; results in input order.
+
+        A chunk that finishes with MS_FINISH_ERROR (no finite logit: SURVEY.md §5 failure
+        row) is re-queued ``retries`` times on its own; the rest of the batch is unaffected.
+        The reference has no retry at all (run_full_evaluation_pipeline.py:627-638)."""
+        tags = [self.submit(p, num_predict, ignore_eos) for p in prompts]
+        order = {t: i for i, t in enumerate(tags)}
+        left = {t: retries for t in tags}
+        out = [None] * len(tags)
+        waiting = set(tags)
+        while waiting:
+            pending = self.step()
+            self.collect()
+            for t, r in self.take(waiting).items():
+                waiting.discard(t)
+                i = order.pop(t)
+                if r.finish == "error" and left[t] > 0:
+                    nt = self.submit(prompts[i], num_predict, ignore_eos)
+                    order[nt], left[nt] = i, left[t] - 1
+                    waiting.add(nt)
+                    pending += 1
+                else:
+                    out[i] = r
+            if pending == 0 and waiting:
+                self.collect()
+                if not any(t in self._mailbox for t in waiting):
+                    raise RuntimeError("engine drained without finishing every request")
+        return out
+
+
+class Engine(RequestQueue):
     def __init__(self, cfg: ModelConfig, device: int = 0, max_batch: int = 8, max_ctx: int = 4096,
                  max_prefill_tokens: int = 16384, n_pages: int = 0, eos_ids=None):
         self.cfg = cfg
@@ -55,6 +114,7 @@ class Engine:
         self.h = h
         self.max_batch, self.max_ctx, self.max_prefill_tokens = max_batch, max_ctx, max_prefill_tokens
         self._next_tag = 1
+        self._mailbox = {}
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -121,21 +181,6 @@ class Engine:
             out.append(Result(int(r.tag), ids, _FINISH.get(r.finish_reason, "error"), int(r.n_prompt)))
         return out
 
-    def generate(self, prompts, num_predict: int, ignore_eos: bool = False) -> list:
-        """Run every prompt (list of id lists) to completion; results in input order."""
-        tags = [self.submit(p, num_predict, ignore_eos) for p in prompts]
-        got = {}
-        while len(got) < len(tags):
-            pending = self.step()
-            for r in self.poll():
-                got[r.tag] = r
-            if pending == 0 and len(got) < len(tags):
-                for r in self.poll():
-                    got[r.tag] = r
-                if len(got) < len(tags):
-                    raise RuntimeError("engine drained without finishing every request")
-        return [got[t] for t in tags]
-
     # ------------------------------------------------------------ probes / stats
     def forward(self, ids, n_layers: int | None = None, hidden: bool = True, logits: bool = False):
         cfg = self.cfg
@@ -164,4 +209,5 @@ class Engine:
         return {"prefill_tokens": s.prefill_tokens, "decode_tokens": s.decode_tokens,
                 "prefill_passes": s.prefill_passes, "decode_steps": s.decode_steps,
                 "finished": s.finished, "prefill_ms": s.prefill_ms, "decode_ms": s.decode_ms,
-                "kernel_ms": list(s.kernel_ms), "kernel_launches": list(s.kernel_launches)}
+                "kernel_ms": list(s.kernel_ms), "kernel_launches": list(s.kernel_launches),
+                "decode_kv_tokens": s.decode_kv_tokens}

@@ -84,13 +84,14 @@ class OllamaShim:
         n = int((req.get("options") or {}).get("num_predict", DEFAULT_NUM_PREDICT))
         t0 = time.perf_counter()
         try:
-            fut = asyncio.run_coroutine_threadsafe(be.agenerate(prompt, n), self.loop)
-            text = fut.result()
+            fut = asyncio.run_coroutine_threadsafe(be.agenerate_full(prompt, n), self.loop)
+            text, finish = fut.result()
         except Exception as e:  # noqa: BLE001 -- reported to the client as Ollama does
             return 500, {"error": str(e)}
         dt = time.perf_counter() - t0
         return 200, {"model": model, "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
-                     "response": text, "done": True, "done_reason": "stop",
+                     "response": text, "done": True,
+                     "done_reason": "length" if finish == "length" else "stop",
                      "total_duration": int(dt * 1e9)}
 
     def start(self):

@@ -115,13 +115,13 @@ class OracleLlama:
             S = k.shape[0]
             kq = np.repeat(k, G, axis=1)  # [S, Hq, D]
             vq = np.repeat(v, G, axis=1)
-            s = np.einsum("thd,shd->hts", q, kq, dtype=np.float32) * scale
+            s = np.matmul(q.transpose(1, 0, 2), kq.transpose(1, 2, 0)) * scale  # [Hq, T, S]
             mask = (np.arange(S)[None, :] > (p0 + np.arange(T))[:, None])
             s = np.where(mask[None], np.float32(-np.inf), s)
             s = s - s.max(axis=-1, keepdims=True)
             p = np.exp(s)
             p = p / p.sum(axis=-1, keepdims=True)
-            o = rnd(np.einsum("hts,shd->thd", p.astype(np.float32), vq, dtype=np.float32))
+            o = rnd(np.matmul(p.astype(np.float32), vq.transpose(1, 0, 2)).transpose(1, 0, 2))  # [T, Hq, D]
             x = x + o.reshape(T, Hq * D) @ L["wo"].T
             xn = rmsnorm(x, L["ffn_norm"], cfg.norm_eps, rnd)
             g = xn @ L["w_gate"].T

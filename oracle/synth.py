@@ -48,8 +48,8 @@ def from_bf16_bits(b: np.ndarray) -> np.ndarray:
     return (np.asarray(b, dtype=np.uint16).astype(np.uint32) << np.uint32(16)).view(np.float32)
 
 
-def _limb_sum(seed: int, kind: int, layer: int, rows: int, cols: int) -> np.ndarray:
-    r = np.arange(rows, dtype=np.uint64)[:, None]
+def _limb_sum(seed: int, kind: int, layer: int, rows: int, cols: int, row0: int = 0) -> np.ndarray:
+    r = np.arange(row0, row0 + rows, dtype=np.uint64)[:, None]
     c = np.arange(cols, dtype=np.uint64)[None, :]
     key = (np.uint64(kind) << np.uint64(58)) | (np.uint64(layer) << np.uint64(50)) | (r << np.uint64(20)) | c
     h = splitmix64(key ^ splitmix64(np.uint64(seed)))
@@ -60,8 +60,13 @@ def _limb_sum(seed: int, kind: int, layer: int, rows: int, cols: int) -> np.ndar
 
 def linear(seed: int, kind: int, layer: int, rows: int, cols: int, std: float) -> np.ndarray:
     scale = np.float32(std * np.sqrt(3.0) / 65536.0)
-    v = _limb_sum(seed, kind, layer, rows, cols).astype(np.float32) * scale
-    return bf16_rne(v)
+    out = np.empty((rows, cols), np.float32)
+    step = max(1, (1 << 22) // cols)  # row blocks: uint64 temporaries stay ~32 MB each
+    for r0 in range(0, rows, step):
+        r1 = min(rows, r0 + step)
+        v = _limb_sum(seed, kind, layer, r1 - r0, cols, row0=r0).astype(np.float32) * scale
+        out[r0:r1] = bf16_rne(v)
+    return out
 
 
 def norm(seed: int, kind: int, layer: int, n: int, jitter: float) -> np.ndarray:

@@ -66,15 +66,27 @@ def test_map_prompt_rendering():
 
 
 # ------------------------------------------------------------------ OllamaLLM mirror
-class FakeEngine:
-    """Test double with libmapsum's request API: each chunk's 'summary' is its last
-    prompt ids reversed (deterministic), so the adapter's plumbing is checkable on CPU."""
+from mapsum.engine import RequestQueue, Result  # noqa: E402
 
-    def __init__(self):
+
+class FakeEngine(RequestQueue):
+    """Test double with libmapsum's request primitives (submit/step/poll); generate(),
+    the mailbox and the one-retry logic are the real RequestQueue's.  Each chunk's
+    'summary' is its last prompt ids reversed (deterministic), so the adapter's plumbing
+    is checkable on CPU.  ``fail_first``: prompts (as tuples) whose first run finishes
+    with "error" (a chunk with a non-finite logit); ``refuse``: prompt lengths submit()
+    rejects (as ms_submit's ENOSPC does)."""
+
+    def __init__(self, fail_first=(), refuse_len=None):
         self.q, self.done, self.steps, self.batches = {}, [], 0, []
         self._tag = 1
+        self._mailbox = {}
+        self.fail_first = set(fail_first)
+        self.refuse_len = refuse_len
 
     def submit(self, ids, n, ignore_eos=False, tag=None):
+        if self.refuse_len is not None and len(ids) > self.refuse_len:
+            raise RuntimeError("libmapsum ms_submit failed (-28): prompt exceeds max_ctx")
         if tag is None:
             tag, self._tag = self._tag, self._tag + 1
         self.q[tag] = (list(ids), n)
@@ -83,21 +95,18 @@ class FakeEngine:
     def step(self):
         self.steps += 1
         self.batches.append(len(self.q))
-        from mapsum.engine import Result
         for tag, (ids, n) in self.q.items():
-            self.done.append(Result(tag, ids[::-1][:n], "length", len(ids)))
+            if tuple(ids) in self.fail_first:
+                self.fail_first.discard(tuple(ids))
+                self.done.append(Result(tag, [], "error", len(ids)))
+            else:
+                self.done.append(Result(tag, ids[::-1][:n], "length", len(ids)))
         self.q = {}
         return 0
 
     def poll(self, cap=256):
         out, self.done = self.done[:cap], self.done[cap:]
         return out
-
-    def generate(self, prompts, num_predict, ignore_eos=False):
-        tags = [self.submit(p, num_predict) for p in prompts]
-        self.step()
-        got = {r.tag: r for r in self.poll()}
-        return [got[t] for t in tags]
 
 
 @pytest.fixture(scope="module")
@@ -161,6 +170,59 @@ def test_ollamallm_engine_error_is_raised(toy_tokenizer):
     with pytest.raises(RuntimeError):
         asyncio.run(m.ainvoke("x"))
     compat._BACKENDS.pop("fake:broken")
+
+
+def test_generate_requeues_a_failed_chunk_once():
+    """a chunk finishing with MS_FINISH_ERROR is re-queued once; the others
+    are not re-run; a second failure is reported for that chunk alone."""
+    eng = FakeEngine(fail_first=[(1, 2, 3)])
+    res = eng.generate([[1, 2, 3], [4, 5]], num_predict=8)
+    assert [r.ids for r in res] == [[3, 2, 1], [5, 4]] and eng.batches == [2, 1]
+    eng = FakeEngine(fail_first=[(7,)])
+    assert eng.generate([[7], [8]], 4, retries=0)[0].finish == "error"
+
+
+def test_generate_leaves_foreign_results_in_the_mailbox():
+    """The synchronous path must not consume (or count) results of requests another
+    caller (the async driver) submitted to the same engine."""
+    eng = FakeEngine()
+    foreign = eng.submit([9, 9, 9], 2, tag=(1 << 40) + 5)
+    res = eng.generate([[1, 2]], 4)
+    assert res[0].ids == [2, 1]
+    assert [r.tag for r in eng.take_where(lambda t: t == foreign)] == [foreign]
+
+
+def test_async_refused_request_fails_alone(toy_tokenizer):
+    """One over-long prompt (ms_submit ENOSPC) fails its own future only; the concurrent
+    requests of the same tick still complete."""
+    eng = FakeEngine(refuse_len=400)
+    compat.register_backend("fake:refuse", compat.MapBackend(eng, toy_tokenizer))
+    m = compat.OllamaLLM("u", "fake:refuse", max_new_tokens=50)
+
+    async def fan_out():
+        return await asyncio.gather(m.ainvoke("ngắn"), m.ainvoke("dài " * 600), m.ainvoke("vừa"),
+                                    return_exceptions=True)
+    try:
+        a, b, c = asyncio.run(fan_out())
+    finally:
+        compat._BACKENDS.pop("fake:refuse", None)
+    assert isinstance(b, RuntimeError) and "refused" in str(b)
+    assert isinstance(a, str) and isinstance(c, str)
+
+
+def test_async_failed_chunk_is_requeued_once(toy_tokenizer):
+    prompt = "Tóm tắt lỗi"
+    be = compat.MapBackend(FakeEngine(), toy_tokenizer)
+    ids = tuple(be.encode_prompt(prompt))
+    be.engine.fail_first = {ids}
+    compat.register_backend("fake:retry", be)
+    m = compat.OllamaLLM("u", "fake:retry", max_new_tokens=1000)
+    try:
+        out = asyncio.run(m.ainvoke(prompt))
+    finally:
+        compat._BACKENDS.pop("fake:retry", None)
+    assert out == clean_thinking_tokens(toy_tokenizer.decode(list(ids)[::-1]))
+    assert be.engine.steps == 2
 
 
 # ------------------------------------------------------------------ chunk sharding

@@ -70,3 +70,13 @@ def test_errors(shim, toy_tokenizer):  # noqa: F811
         r = requests.post(f"http://127.0.0.1:{s.port}/api/generate",
                           json={"model": "m", "prompt": "x", "stream": False}, timeout=10)
         assert r.status_code == 500 and "device lost" in r.json()["error"]
+
+
+def test_done_reason_reports_truncation(shim):
+    """Ollama answers done_reason "length" when num_predict cut the output, "stop" at EOS
+    (the FakeEngine finishes every chunk with "length")."""
+    url, _, _ = shim
+    payload = {"model": "llama3.2:3b", "prompt": "Tóm tắt", "stream": False, "options": {"num_predict": 3}}
+    r = requests.post(f"{url}/api/generate", json=payload, timeout=30)
+    r.raise_for_status()
+    assert r.json()["done_reason"] == "length"
