@@ -196,8 +196,9 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 // in flight before its first MFMA.  The G query heads of the kv head are MFMA columns
 // 0..G-1.  Per-wave (m, l, O^T) are merged in LDS (reusing the waves' V images); each block
 // writes one partial (m, l, o[128]) per (b, q head, split), and the LAST block of a
-// (b, kv head) to finish (agent-scope release/acquire ticket, cdna_hip_programming.md §6
-// Guideline 16) combines the nsplit partials and writes the bf16 output -- no second launch.
+// (b, kv head) to finish (arrival counter with write-through partials,
+// cdna_hip_programming.md §6 Guideline 16) combines the nsplit partials and writes the bf16
+// output -- no second launch.
 //
 // FROM_SLABS (the fused decode chain): the QKV projection arrives as S fp32 split-K slabs
 // [S][B][(Hq+2Hk)*128] with Q/K rows rope-permuted (k_gemv.hip).  The prologue adds the
@@ -219,6 +220,8 @@ constexpr int kMaxSplits = 127;
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
   return (size_t)kMaxTickets * 4 + (size_t)B * Hq * decode_nsplit(max_len) * 132 * sizeof(float);
 }
+
+size_t attn_decode_ticket_bytes() { return (size_t)kMaxTickets * 4; }
 
 bool attn_decode_supported(int B, int Hq, int Hk, int max_len) {
   return Hk >= 1 && Hq % Hk == 0 && Hq / Hk <= kMaxGroup && B * Hk <= kMaxTickets &&
@@ -418,37 +421,27 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
     }
     const int hq = kvh * G + c;
     float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;
-    dst[k] = (k == 0) ? M : acc;
+    if constexpr (FUSED_COMBINE)
+      st_sc1(dst + k, (k == 0) ? M : acc);  // write-through: read by the last arriver below
+    else
+      dst[k] = (k == 0) ? M : acc;
   }
 
   // ---- in-launch combine: the last of the nsplit blocks of (b, kvh) merges the partials
+  // (Guideline 16 counter form with write-through partials: no fences; the counters are
+  // zeroed by a memset node ahead of the launch, and reset by the last arriver)
   if constexpr (!FUSED_COMBINE) return;
-  wait_vmcnt0();    // every storing wave: its partial stores have completed
-  __syncthreads();
   unsigned* flag = (unsigned*)(smem + 4 * 16384);  // reuse qn (consumed)
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    wait_vmcnt0();
-    const unsigned t = __hip_atomic_fetch_add(&tickets[b * Hk + kvh], 1u, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT);
-    const bool last = t == (unsigned)nsplit - 1;
-    if (last) {
-      __hip_atomic_store(&tickets[b * Hk + kvh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      wait_vmcnt0();
-    }
-    *flag = last ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*flag == 0u) return;
+  if (!arrive_last(&tickets[b * Hk + kvh], (unsigned)nsplit, flag)) return;
+  if (tid == 0) __hip_atomic_store(&tickets[b * Hk + kvh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // split weights per q head: f_s = 2^(m_s - max m), L = sum_s f_s l_s (split order)
   float* ml = (float*)smem;                           // [G][128] m_s, then [G][128] l_s
   float* wsum = ml + 2 * kMaxGroup * 128;             // [G][128] f_s, [c][127] = L
   for (int e = tid; e < G * nsplit; e += 256) {       // every (head, split) load in parallel
     const int c = e / nsplit, s_ = e - c * nsplit;
     const float* p = ws + (((size_t)b * Hq + kvh * G + c) * nsplit + s_) * 132;
-    ml[c * 128 + s_] = p[0];
-    ml[(kMaxGroup + c) * 128 + s_] = p[1];
+    ml[c * 128 + s_] = ld_sc1(p);
+    ml[(kMaxGroup + c) * 128 + s_] = ld_sc1(p + 1);
   }
   __syncthreads();
   for (int c = tid; c < G; c += 256) {
@@ -472,11 +465,11 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
     if (nsplit <= 16) {  // clamped indices, no branches: all loads in flight at once
       float ov[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) ov[q] = p[min(q, nsplit - 1) * 132];
+      for (int q = 0; q < 16; ++q) ov[q] = ld_sc1(p + min(q, nsplit - 1) * 132);
 #pragma unroll
       for (int q = 0; q < 16; ++q) O += (q < nsplit) ? f[q] * ov[q] : 0.f;
     } else {
-      for (int q = 0; q < nsplit; ++q) O += f[q] * p[q * 132];
+      for (int q = 0; q < nsplit; ++q) O += f[q] * ld_sc1(p + q * 132);
     }
     out[(size_t)b * Hq * kHeadDim + (kvh * G + c) * kHeadDim + d] = f2bf(O / f[127]);
   }

@@ -340,10 +340,13 @@ def test_errors_are_reported(dev):
         e.close()
 
 
-@pytest.mark.parametrize("slabs,fused", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
-    """The decode-attention variants (q/k/v from QKV split slabs or from the GEMV RoPE
-    epilogue; split combine in-launch or as a second launch) all agree with the oracle."""
+@pytest.mark.parametrize("chain,slabs,fused", [(1, 1, 1), (0, 0, 0), (0, 0, 1), (0, 1, 0), (0, 1, 1)])
+def test_decode_attention_variants(oracle, monkeypatch, chain, slabs, fused):
+    """The decode variants -- the chain (RMSNorm in the projections' staging, split-K slabs
+    folded in-launch, attention split combine in-launch, argmax partials in the lm_head
+    epilogue) and the older launch sequences (q/k/v from QKV split slabs or from the GEMV
+    RoPE epilogue; split combine in-launch or as a second launch) -- all agree with the oracle."""
+    monkeypatch.setenv("MS_CHAIN", str(chain))
     monkeypatch.setenv("MS_ATTN_SLABS", str(slabs))
     monkeypatch.setenv("MS_ATTN_FUSED_COMBINE", str(fused))
     e = Engine(TINY, device=0, max_batch=6, max_ctx=1024, max_prefill_tokens=4096)
