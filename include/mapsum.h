@@ -166,6 +166,9 @@ int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run
 #define MS_EPI_ADD_F32 1     /* out fp32 [M][ldo] += acc  (residual add)       */
 #define MS_EPI_SWIGLU 2      /* W rows interleaved gate/up per 16; out bf16 [M][N/2] */
 #define MS_EPI_STORE_F32 3   /* out fp32 [M][ldo]                              */
+#define MS_EPI_ARGMAX 5      /* decode GEMV only: out {max, id} float2 [M][ldo = N/16], one per
+                                16-column tile (ties -> lowest id; NaN never wins); finish the
+                                rows with ms_op_argmax_partials                          */
 /* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0 */
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* stream);
@@ -200,8 +203,10 @@ int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows,
 /* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
                   const int32_t* row_idx, void* stream);
-/* ids[r] = argmax_j logits[r][j] (ties -> lowest j) */
+/* ids[r] = argmax_j logits[r][j] (ties -> lowest j; -1 when no logit of the row is finite) */
 int ms_op_argmax(const void* logits, int32_t rows, int32_t n, int32_t* ids, void* stream);
+/* ids[r] = the lowest id of the largest {max, id} partial of row r (MS_EPI_ARGMAX output) */
+int ms_op_argmax_partials(const void* partials, int32_t rows, int32_t tiles, int32_t* ids, void* stream);
 
 #ifdef __cplusplus
 }

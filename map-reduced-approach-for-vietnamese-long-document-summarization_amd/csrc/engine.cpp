@@ -36,7 +36,6 @@ using namespace ms;
 namespace {
 
 thread_local std::string g_last_error;
-constexpr int kFoldTickets = 1024;  // column tiles of one FOLD projection (N/16 <= 16384)
 
 struct MsError : std::runtime_error {
   int code;
@@ -111,13 +110,6 @@ struct ms_engine {
   // decode O / down projections: split-K partial slabs [S][B][H] fp32, folded into the
   // residual by the next residual_rmsnorm launch (pending_split = S of the unfolded slabs)
   float* slabs = nullptr;
-  // decode chain (use_chain): the residual x stays fp32 and current -- split-K O / down
-  // projections fold their slabs into it in-launch (FOLD epilogue) and leave per-16-column
-  // sums of squares in ssq [B][H/16]; the next projection normalises in its X staging (NORM
-  // prologue).  fold_tickets: one arrival counter per column tile.
-  float* ssq = nullptr;
-  unsigned* fold_tickets = nullptr;
-  bool use_chain = true;
   int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
   int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
@@ -290,80 +282,9 @@ struct ms_engine {
     pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down);
   }
 
-  // ---- decode chain ---------------------------------------------------------------
-  bool chain_decode(int B) const {
-    return use_chain && attn_slabs && fused_decode(B) && gemv_norm_supported(B, H / std::max(split_qkv, 1)) &&
-           gemv_split_supported(B, QKVN, H, std::max(split_qkv, 1));
-  }
-  GemvArgs norm_args(const bf16_t* g) const {
-    GemvArgs ga{};
-    ga.nx = x;
-    ga.nssq = ssq;
-    ga.ng = g;
-    ga.nP = H / 16;
-    ga.neps = cfg.norm_eps;
-    return ga;
-  }
-  GemvArgs fold_args() const {
-    GemvArgs ga{};
-    ga.fx = x;
-    ga.fssq = ssq;
-    ga.tickets = fold_tickets;
-    return ga;
-  }
-  // split-K projection into slabs with the chain's prologue / epilogue options; returns S
-  int proj_split_chain(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S,
-                       const GemvArgs& ga) {
-    prof_begin(K_GEMV);
-    int used = 1;
-    if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
-      int Sq = qsplit > 0 ? qsplit : S;
-      if (!(Sq >= 1 && Sq <= kMaxSplit && qgemv_split_supported(M, N, K, Sq))) Sq = 1;
-      launch_qgemv_split(X, q->m, slabs, M, N, K, Sq, stream, &ga);
-      used = Sq;
-    } else {
-      if (!(S >= 1 && S <= kMaxSplit && gemv_split_supported(M, N, K, S))) S = 1;
-      launch_gemv_split_ex(X, W, slabs, M, N, K, S, &ga, stream);
-      used = S;
-    }
-    prof_end(K_GEMV);
-    return used;
-  }
-  // the consumer of the folded residual: RMSNorm in its prologue when its X image fits LDS,
-  // else a standalone RMSNorm into xb first (returns the prologue arguments or null)
-  const GemvArgs* norm_or_stage(GemvArgs& ga, const bf16_t* g, int B, int K) {
-    ga = norm_args(g);
-    if (gemv_norm_supported(B, K)) return &ga;
-    prof_begin(K_MISC);
-    launch_rmsnorm(x, g, xb, B, H, cfg.norm_eps, nullptr, stream);
-    prof_end(K_MISC);
-    return nullptr;
-  }
-  void run_layer_chain(int l, int B, const DecodeAttnArgs& da) {
-    const Layer& Ly = layers[l];
-    KVView kv = kv_layer(l);
-    const auto& Q = lq[l];
-    const GemvArgs qn = norm_args(Ly.attn_norm);  // chain_decode() checked the QKV image fits
-    DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab};
-    qa.S = proj_split_chain(&Q[QS_QKV], nullptr, Ly.wqkv, B, QKVN, H, split_qkv, qn);
-    prof_begin(K_ATTN_DECODE);
-    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, /*fused_combine=*/true);
-    prof_end(K_ATTN_DECODE);
-    const GemvArgs fo = fold_args();
-    proj_split_chain(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, fo);
-    GemvArgs gn;
-    const GemvArgs* gp = norm_or_stage(gn, Ly.ffn_norm, B, H);
-    proj(&Q[QS_GU], gp ? nullptr : xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, gp, K_GEMV);
-    proj_split_chain(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down, fo);
-  }
-
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
   void run_layer(int l, int T, bool decode, const int32_t* tok_pos, const int32_t* tok_slot,
                  const PrefillAttnArgs& pa, const DecodeAttnArgs& da) {
-    if (decode && chain_decode(T)) {
-      run_layer_chain(l, T, da);
-      return;
-    }
     if (decode && fused_decode(T)) {
       run_layer_fused_decode(l, T, tok_pos, tok_slot, da);
       return;
@@ -549,9 +470,6 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
                                        true);  // zeroed: split-combine tickets
     E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * ms_engine::kMaxSlabRows * std::max(E.QKVN, E.H));
-    E.ssq = E.dalloc<float>((size_t)cfg->max_batch * (E.H / 16), true);
-    E.fold_tickets = E.dalloc<unsigned>(kFoldTickets, true);
-    if (const char* v = getenv("MS_CHAIN")) E.use_chain = atoi(v) != 0;
     if (const char* v = getenv("MS_SPLIT_QKV")) E.split_qkv = atoi(v);
     if (const char* v = getenv("MS_ATTN_SLABS")) E.attn_slabs = atoi(v) != 0;
     if (const char* v = getenv("MS_ATTN_FUSED_COMBINE")) E.attn_fused_combine = atoi(v) != 0;
@@ -982,40 +900,27 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
 static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& da) {
   const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
   PrefillAttnArgs pa{};
-  if (E.chain_decode(B)) {
-    // counters of the in-launch hand-offs start at zero every step (memset nodes)
-    HIP_OK(hipMemsetAsync(E.fold_tickets, 0, kFoldTickets * sizeof(unsigned), E.stream));
-    HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
-    E.prof_begin(K_MISC);
-    launch_embed_ssq(d + o_ids, B, E.embed, E.H, E.x, E.ssq, E.stream);
-    E.prof_end(K_MISC);
-    for (int l = 0; l < E.L; ++l) E.run_layer_chain(l, B, da);
-    GemvArgs gn;
-    const GemvArgs* gp = E.norm_or_stage(gn, E.final_norm, B, E.H);
-    const bf16_t* X = gp ? nullptr : E.xb;
-    const int tiles = E.V / 16;  // {max, id} partials [B][tiles] in the logits buffer
-    if (E.lmq.ready() && qgemv_supported(B, E.V, E.H, MS_GEMV_EPI_ARGMAX))
-      E.proj(&E.lmq, X, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, gp, K_LMHEAD);
-    else
-      E.proj(nullptr, X, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, gp, K_LMHEAD);
-    E.prof_begin(K_MISC);
-    launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
-    E.prof_end(K_MISC);
-    return;
-  }
+  // in-launch split-combine counters start at zero every step (a memset node)
+  HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
   E.prof_begin(K_MISC);
   launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
   E.prof_end(K_MISC);
   E.pending_split = 0;
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   E.residual_norm(E.final_norm, B);  // folds the last layer's down slabs (if fused)
-  if (E.lmq.ready() && qgemv_supported(B, E.V, E.H, MS_GEMV_EPI_STORE_F32))
-    E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_GEMV_EPI_STORE_F32, nullptr, K_LMHEAD);
-  else
+  if (gemv_supported(B, E.V, E.H, MS_GEMV_EPI_ARGMAX)) {
+    // greedy argmax in the lm_head epilogue: {max, id} per 16-column tile, no logits row
+    const int tiles = E.V / 16;
+    E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, nullptr, K_LMHEAD);
+    E.prof_begin(K_MISC);
+    launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
+    E.prof_end(K_MISC);
+  } else {
     E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
-  E.prof_begin(K_MISC);
-  launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
-  E.prof_end(K_MISC);
+    E.prof_begin(K_MISC);
+    launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
+    E.prof_end(K_MISC);
+  }
 }
 
 // one greedy decode step for every running sequence (B rows of one token each)
@@ -1268,7 +1173,8 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
                      int32_t ldo, int32_t epi, void* ws, int32_t waves, void* stream) {
   return op_guard([&] {
     REQUIRE(X && W && out && ws && N >= 16 && N % 16 == 0, MS_EINVAL, "bad gemv operands");
-    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0),
+            MS_EINVAL, "bad epilogue");
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
     launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
                    (hipStream_t)stream);
@@ -1354,6 +1260,13 @@ int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t h
     REQUIRE(x && w && y && rows >= 1 && hidden >= 4 && hidden % 4 == 0, MS_EINVAL, "bad rmsnorm shape");
     launch_rmsnorm((const float*)x, (const bf16_t*)w, (bf16_t*)y, rows, hidden, eps, row_idx,
                    (hipStream_t)stream);
+  });
+}
+
+int ms_op_argmax_partials(const void* partials, int32_t rows, int32_t tiles, int32_t* ids, void* stream) {
+  return op_guard([&] {
+    REQUIRE(partials && ids && rows >= 1 && tiles >= 1, MS_EINVAL, "bad argmax_partials shape");
+    launch_argmax_partials(partials, rows, tiles, ids, (hipStream_t)stream);
   });
 }
 

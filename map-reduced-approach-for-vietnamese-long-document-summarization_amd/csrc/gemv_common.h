@@ -18,42 +18,6 @@ __device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restric
   }
 }
 
-// Decode-chain RMSNorm prologue: the block's X image [M][K] (K range [koff, koff+K) of rows
-// of length H) is bf16((x * rinv) * g), the arithmetic of rmsnorm_kernel, with rinv from the
-// nP fixed-order partial sums of squares of the row (deterministic, independent of M and of
-// the other rows).  rinv lands after the X image; caller synchronises.
-__device__ __forceinline__ void gemv_stage_x_norm(char* smem, const GemvArgs& ga, int M, int K, int H,
-                                                  int koff) {
-  const size_t xstride = 2 * (size_t)K + 16;
-  float* rinv_s = (float*)(smem + (size_t)M * xstride);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int r = wave; r < M; r += nw) {
-    const float* p = ga.nssq + (size_t)r * ga.nP;
-    float a = 0.f;
-    for (int t = lane; t < ga.nP; t += 64) a += p[t];
-    a = wave_sum(a);
-    if (lane == 0) rinv_s[r] = 1.0f / sqrtf(a / (float)H + ga.neps);
-  }
-  __syncthreads();
-  const int kch = K / 8;
-#pragma unroll 2
-  for (int c = threadIdx.x; c < M * kch; c += blockDim.x) {
-    const int r = c / kch, k = koff + (c - r * kch) * 8;
-    const float* xr = ga.nx + (size_t)r * H + k;
-    const float4 a = *(const float4*)xr, b = *(const float4*)(xr + 4);
-    const uint4 g = ldg16(ga.ng + k);
-    const float rv = rinv_s[r];
-    uint4 o;
-    o.x = pack2bf((a.x * rv) * __uint_as_float(g.x << 16), (a.y * rv) * __uint_as_float(g.x & 0xFFFF0000u));
-    o.y = pack2bf((a.z * rv) * __uint_as_float(g.y << 16), (a.w * rv) * __uint_as_float(g.y & 0xFFFF0000u));
-    o.z = pack2bf((b.x * rv) * __uint_as_float(g.z << 16), (b.y * rv) * __uint_as_float(g.z & 0xFFFF0000u));
-    o.w = pack2bf((b.z * rv) * __uint_as_float(g.w << 16), (b.w * rv) * __uint_as_float(g.w & 0xFFFF0000u));
-    *(uint4*)(smem + r * xstride + (c - r * kch) * 16) = o;
-  }
-}
-
-inline size_t gemv_norm_lds_extra() { return 64 * sizeof(float); }
-
 __device__ __forceinline__ void amax_merge_dev(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }
@@ -142,36 +106,6 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
       for (int o = 4; o < 64; o <<= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
       if ((l & 15) == 0 && row < M)
         ((float2*)out)[(size_t)row * ldo + blockIdx.x] = make_float2(v, __int_as_float(idx));
-    }
-  } else if constexpr (EPI == MS_GEMV_EPI_FOLD) {
-    static_assert(NT == 1, "fold epilogue works on 16-column tiles");
-    // 1. this block's slab, write-through
-    for (int e = tid; e < ELEMS; e += nthreads) {
-      const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
-      const int row = m * 16 + 4 * (l >> 4) + j, col = n0 + (l & 15);
-      if (row < M && col < N) st_sc1((float*)out + (size_t)row * ldo + col, sum_e(e));
-    }
-    // 2. the last of the tile's S blocks folds the S slabs into the residual (slab order:
-    //    residual_rmsnorm_kernel's arithmetic) and writes the tile's sums of squares
-    if (!arrive_last(ga.tickets + blockIdx.x, gridDim.y, (unsigned*)red + nw * ELEMS)) return;
-    if (tid == 0)  // ready for the next launch (a memset node also zeroes them every step)
-      __hip_atomic_store((gu32_t*)(ga.tickets + blockIdx.x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const float* slab0 = (const float*)out - (size_t)blockIdx.y * M * ldo;
-    const size_t sstride = (size_t)M * ldo;
-    for (int e = tid; e < M * 16; e += nthreads) {  // 16 consecutive lanes per row
-      const int row = e >> 4, col = n0 + (e & 15);
-      const float* sp = slab0 + (size_t)row * ldo + col;
-      float acc = ld_sc1(sp);
-      for (int q = 1; q < (int)gridDim.y; ++q) acc += ld_sc1(sp + q * sstride);
-      float* xp = ga.fx + (size_t)row * ldo + col;
-      const float xv = *xp + acc;
-      *xp = xv;
-      float sq = xv * xv;
-      sq += __shfl_xor(sq, 8, 64);
-      sq += __shfl_xor(sq, 4, 64);
-      sq += __shfl_xor(sq, 2, 64);
-      sq += __shfl_xor(sq, 1, 64);
-      if ((e & 15) == 0) ga.fssq[(size_t)row * gridDim.x + blockIdx.x] = sq;
     }
   } else {
     for (int e = tid; e < ELEMS; e += nthreads) {

@@ -57,18 +57,16 @@ constexpr size_t kMaxLds = 160 * 1024;
 
 // staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of a
 // fragment read on different banks); rows >= M alias row M-1 and are never stored.
-static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds, bool norm = false) {
-  size_t xs = xlds ? (size_t)M * (2 * (size_t)K + 16) + (norm ? gemv_norm_lds_extra() : 0) : 0;
-  const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4 + 16;  // per-wave partials + a flag
+static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
+  size_t xs = xlds ? (size_t)M * (2 * (size_t)K + 16) : 0;
+  const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;  // per-wave partials
   return xs > red ? xs : red;
 }
-
-__host__ __device__ constexpr bool split_epi(int epi) { return epi == MS_GEMV_EPI_STORE_F32 || epi == MS_GEMV_EPI_FOLD; }
 
 // Split-K (gridDim.y = S > 1, STORE_F32 only): block (x, y) covers k in [y*K, (y+1)*K) of
 // rows of length ldk and writes its fp32 partial to slab y = out + y*M*ldo; the consumer
 // (residual_rmsnorm_kernel) adds the S slabs in slab order -- deterministic, no atomics.
-template <int MT, int NT, int EPI, int U, bool XL, bool NORM>
+template <int MT, int NT, int EPI, int U, bool XL>
 __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
@@ -78,7 +76,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * 16 * NT;
   const int kbeg = wave * U * 64;
-  if constexpr (split_epi(EPI)) {
+  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
     X += (size_t)blockIdx.y * K;
     W += (size_t)blockIdx.y * K;
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
@@ -98,10 +96,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
   // 2. stage the M rows of X into LDS (XL) -- or read fragments from L2 (large M*K)
   const size_t xstride = 2 * (size_t)K + 16;
   if constexpr (XL) {
-    if constexpr (NORM)  // decode chain: X = RMSNorm of the fp32 residual, in the staging
-      gemv_stage_x_norm(smem, ga, M, K, ldk, split_epi(EPI) ? (int)blockIdx.y * K : 0);
-    else
-      gemv_stage_x(smem, X, M, K, ldk);
+    gemv_stage_x(smem, X, M, K, ldk);
     __syncthreads();
   }
 
@@ -143,15 +138,12 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
-    if (xl && ga.nx)
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true, true>), grid, blk, lds, s, X, W, out, M,
-                N, K, ldk, ldo, ga);
-    else if (xl)
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true, false>), grid, blk, lds, s, X, W, out, M,
-                N, K, ldk, ldo, ga);
+    if (xl)
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+                ldo, ga);
     else
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, false, false>), grid, blk, lds, s, X, W, out,
-                M, N, K, ldk, ldo, ga);
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+                ldo, ga);
   }
 }
 
@@ -184,7 +176,6 @@ static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N
     case MS_GEMV_EPI_SWIGLU: GE(2, MS_GEMV_EPI_SWIGLU); break;
     case MS_GEMV_EPI_ROPE_KV: GE(1, MS_GEMV_EPI_ROPE_KV); break;
     case MS_GEMV_EPI_ARGMAX: GE(1, MS_GEMV_EPI_ARGMAX); break;
-    case MS_GEMV_EPI_FOLD: GE(1, MS_GEMV_EPI_FOLD); break;
     default: GE(1, MS_GEMV_EPI_STORE_F32); break;
   }
 #undef GE
@@ -193,7 +184,7 @@ static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N
 bool gemv_supported(int M, int N, int K, int epi) {
   if (M < 1 || M > 64 || K % 64) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
-  if ((epi == MS_GEMV_EPI_ARGMAX || epi == MS_GEMV_EPI_FOLD) && N % 16) return false;
+  if (epi == MS_GEMV_EPI_ARGMAX && N % 16) return false;
   const GemvPlan p = gemv_plan(M, N, K, epi);
   if (p.waves == 0) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && gemv_lds_bytes(p, M, K, true) > kMaxLds) return false;
@@ -206,13 +197,11 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   if (M <= 0) return;
   const GemvPlan p = gemv_plan(M, N, K, epi, force_waves);
   if (p.waves == 0) return;  // callers check gemv_supported()
+  const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
+  const size_t lds = gemv_lds_bytes(p, M, K, xl);
+  if (lds > kMaxLds) return;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
-  const bool norm = ga.nx != nullptr;
-  const bool xl = gemv_lds_bytes(p, M, K, true, norm) <= kMaxLds;
-  if (norm && !xl) return;  // callers check gemv_norm_supported()
-  const size_t lds = gemv_lds_bytes(p, M, K, xl, norm);
-  if (lds > kMaxLds) return;
   switch (p.MT) {
     case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
     case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
@@ -236,43 +225,39 @@ void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, in
   gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, nullptr, force_waves, s);
 }
 
-void launch_gemv_split_ex(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
-                          const GemvArgs* ga, hipStream_t s) {
-  const int epi = (ga && ga->fx) ? MS_GEMV_EPI_FOLD : MS_GEMV_EPI_STORE_F32;
-  gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, epi, ga, 0, s);
-}
-
-bool gemv_norm_supported(int M, int K) {
-  return M >= 1 && M <= 64 && (size_t)M * (2 * (size_t)K + 16) + gemv_norm_lds_extra() <= kMaxLds;
-}
-
 // ---------------------------------------------------------------- argmax of partials
 // rows of {max, id} float2 partials (MS_GEMV_EPI_ARGMAX) -> greedy ids; ties -> lowest id
 // whatever the merge order; -1 when the row has no finite maximum (a failed chunk)
-__global__ __launch_bounds__(256) void argmax_partials_kernel(const float2* __restrict__ part, int tiles,
-                                                              int32_t* __restrict__ out) {
-  __shared__ float sv[4];
-  __shared__ int si[4];
+__global__ __launch_bounds__(1024) void argmax_partials_kernel(const float2* __restrict__ part, int tiles,
+                                                               int32_t* __restrict__ out) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
   const float2* p = part + (size_t)blockIdx.x * tiles;
   float v = -INFINITY;
   int idx = 0x7FFFFFFF;
-  for (int t = threadIdx.x; t < tiles; t += 256) {
-    const float2 q = p[t];
-    amax_merge_dev(v, idx, q.x, __float_as_int(q.y));
+  for (int t0 = 0; t0 < tiles; t0 += 8 * 1024) {  // 8 loads in flight per thread
+    float2 q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = t0 + i * 1024 + threadIdx.x;
+      q[i] = t < tiles ? p[t] : make_float2(-INFINITY, __int_as_float(0x7FFFFFFF));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax_merge_dev(v, idx, q[i].x, __float_as_int(q[i].y));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
   if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; si[threadIdx.x >> 6] = idx; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < 4; ++w) amax_merge_dev(v, idx, sv[w], si[w]);
+    for (int w = 1; w < 16; ++w) amax_merge_dev(v, idx, sv[w], si[w]);
     out[blockIdx.x] = (idx == 0x7FFFFFFF || !__builtin_isfinite(v)) ? -1 : idx;
   }
 }
 
 void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* out, hipStream_t s) {
   if (rows <= 0) return;
-  MS_LAUNCH(argmax_partials_kernel, dim3(rows), dim3(256), 0, s, (const float2*)partials, tiles, out);
+  MS_LAUNCH(argmax_partials_kernel, dim3(rows), dim3(1024), 0, s, (const float2*)partials, tiles, out);
 }
 
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,

@@ -36,38 +36,6 @@ void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x,
   MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
 }
 
-// decode chain: the embedding rows plus, per 16-column tile, the sum of squares the first
-// layer's RMSNorm prologue (gemv_stage_x_norm) reduces -- the layout the FOLD epilogue writes
-__global__ __launch_bounds__(256) void embed_ssq_kernel(const int32_t* __restrict__ ids,
-                                                        const bf16_t* __restrict__ emb, int H,
-                                                        float* __restrict__ x, float* __restrict__ ssq) {
-  const int t = blockIdx.x;
-  const bf16_t* row = emb + (size_t)ids[t] * H;
-  float* xo = x + (size_t)t * H;
-  for (int c = threadIdx.x; c < H / 16; c += blockDim.x) {
-    const uint4 v0 = *(const uint4*)(row + c * 16), v1 = *(const uint4*)(row + c * 16 + 8);
-    const uint32_t w[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-    float f[16];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      f[2 * i] = __uint_as_float(w[i] << 16);
-      f[2 * i + 1] = __uint_as_float(w[i] & 0xFFFF0000u);
-    }
-    float sq = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sq += f[i] * f[i];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) *(float4*)(xo + c * 16 + 4 * i) = make_float4(f[4 * i], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]);
-    ssq[(size_t)t * (H / 16) + c] = sq;
-  }
-}
-
-void launch_embed_ssq(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, float* ssq,
-                      hipStream_t s) {
-  if (T <= 0) return;
-  MS_LAUNCH(embed_ssq_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x, ssq);
-}
-
 // ---------------------------------------------------------------- RMSNorm
 // y = bf16( (x * rsqrt(mean(x^2) + eps)) * w ), one 256-thread block per row; the row is
 // read once (<= 8 float4 per thread kept in registers, H <= 8192).

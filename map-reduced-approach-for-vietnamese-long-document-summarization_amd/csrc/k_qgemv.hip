@@ -161,7 +161,7 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 //         weights h*128 + {0,32,64,96} + l.
 // MFMA t of a super-block takes 8 of those weights per lane and the X elements of the
 // same k -- a k permutation applied to both operands, so every dot product is unchanged.
-template <int MT, int NT, int EPI, int SBW, bool XL, bool NORM>
+template <int MT, int NT, int EPI, int SBW, bool XL>
 __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, GemvArgs ga) {
@@ -169,8 +169,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
   // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
   // of the full row, where K is the per-split length; X and out shift to that slab.
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
-  constexpr bool SPLIT = EPI == MS_GEMV_EPI_STORE_F32 || EPI == MS_GEMV_EPI_FOLD;
-  if constexpr (SPLIT) {
+  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
     X += (size_t)blockIdx.y * K;
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
   }
@@ -203,10 +202,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         q1[j][n] = ldg16(bp + 32 + 32 * g);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      if constexpr (NORM)
-        gemv_stage_x_norm(smem, ga, M, K, ldx, SPLIT ? (int)blockIdx.y * K : 0);
-      else
-        gemv_stage_x(smem, X, M, K, ldx);
+      gemv_stage_x(smem, X, M, K, ldx);
       __syncthreads();
     }
 #pragma unroll
@@ -261,10 +257,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      if constexpr (NORM)
-        gemv_stage_x_norm(smem, ga, M, K, ldx, SPLIT ? (int)blockIdx.y * K : 0);
-      else
-        gemv_stage_x(smem, X, M, K, ldx);
+      gemv_stage_x(smem, X, M, K, ldx);
       __syncthreads();
     }
 #pragma unroll
@@ -326,13 +319,11 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
 
 static constexpr size_t kLdsCap = 160 * 1024;
 
-static bool qx_in_lds(int M, int K, bool norm = false) {
-  return (size_t)M * (2 * (size_t)K + 16) + (norm ? gemv_norm_lds_extra() : 0) <= kLdsCap;
-}
+static bool qx_in_lds(int M, int K) { return (size_t)M * (2 * (size_t)K + 16) <= kLdsCap; }
 
-static size_t qlds(const QPlan& p, int M, int K, bool norm = false) {
-  const size_t xs = qx_in_lds(M, K, norm) ? (size_t)M * (2 * (size_t)K + 16) + (norm ? gemv_norm_lds_extra() : 0) : 0;
-  const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4 + 16;  // partials + a flag word
+static size_t qlds(const QPlan& p, int M, int K) {
+  const size_t xs = qx_in_lds(M, K) ? (size_t)M * (2 * (size_t)K + 16) : 0;
+  const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
 
@@ -346,22 +337,18 @@ bool qgemv_supported(int M, int N, int K, int epi) {
 template <int MT, int NT, int EPI>
 static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
                      const QPlan& p, const GemvArgs& ga, hipStream_t s, int S = 1) {
-  const bool norm = ga.nx != nullptr;
-  const size_t lds = qlds(p, M, K, norm);
+  const size_t lds = qlds(p, M, K);
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;
   } else {
-    const bool xl = qx_in_lds(M, K, norm);
-    if (norm && !xl) return;  // callers check gemv_norm_supported()
-#define QL(SBW_, XL_, NORM_) \
-    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XL_, NORM_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
-    if (p.SBW == 2 && norm) QL(2, true, true);
-    else if (p.SBW == 2 && xl) QL(2, true, false);
-    else if (p.SBW == 2) QL(2, false, false);
-    else if (norm) QL(1, true, true);
-    else if (xl) QL(1, true, false);
-    else QL(1, false, false);
+    const bool xl = qx_in_lds(M, K);
+#define QL(SBW_, XL_) \
+    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XL_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
+    if (p.SBW == 2 && xl) QL(2, true);
+    else if (p.SBW == 2) QL(2, false);
+    else if (xl) QL(1, true);
+    else QL(1, false);
 #undef QL
   }
 }
@@ -402,23 +389,18 @@ bool qgemv_split_supported(int M, int N, int K, int S) {
 // fp32 partial slabs [S][M][N] over S equal K ranges (super-block aligned); the caller
 // folds them (residual_rmsnorm_kernel / the decode attention prologue)
 void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
-                        hipStream_t s, const GemvArgs* ga_in) {
+                        hipStream_t s) {
   if (M <= 0) return;
   const int Ks = K / S;
   const QPlan p = qplan(M, N, Ks, MS_GEMV_EPI_STORE_F32);
   if (p.waves == 0) return;  // callers check qgemv_split_supported()
-  GemvArgs ga{};
-  if (ga_in) ga = *ga_in;
-#define QS(MT_) \
-  (ga.fx ? qgemv_go<MT_, 1, MS_GEMV_EPI_FOLD>(X, q, slabs, M, N, Ks, N, p, ga, s, S) \
-         : qgemv_go<MT_, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S))
+  const GemvArgs ga{};
   switch (p.MT) {
-    case 1: QS(1); break;
-    case 2: QS(2); break;
-    case 3: QS(3); break;
-    default: QS(4); break;
+    case 1: qgemv_go<1, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    case 2: qgemv_go<2, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    case 3: qgemv_go<3, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
+    default: qgemv_go<4, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
   }
-#undef QS
 }
 
 }  // namespace ms

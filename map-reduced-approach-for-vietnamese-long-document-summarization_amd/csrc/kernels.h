@@ -55,10 +55,7 @@ enum {
   MS_GEMV_EPI_ROPE_KV = 4,
   // greedy argmax partials: out = {max, id} float2 [M][tiles] of each 16-column tile
   // (ties -> lowest id, NaN never wins); launch_argmax_partials finishes the rows
-  MS_GEMV_EPI_ARGMAX = 5,
-  // split-K fp32 slabs + in-launch fold: the last of a column tile's S blocks adds the S
-  // slabs (slab order) to the fp32 residual and writes the tile's sum of squares
-  MS_GEMV_EPI_FOLD = 6
+  MS_GEMV_EPI_ARGMAX = 5
 };
 struct GemvArgs {
   // ROPE_KV epilogue: Q -> out[row][h*128..] (ld = ldo), K/V -> paged cache
@@ -68,36 +65,15 @@ struct GemvArgs {
   const float* sin_tab;
   KVView kv;
   int Hq, Hk;
-  // RMSNorm prologue (decode chain; nx != null): the GEMV's X is bf16((nx*rinv)*ng), rinv =
-  // 1/sqrt(sum/H + eps) with sum = the fixed-order sum of the row's nP per-16-column sums
-  // of squares nssq[row][0..nP) (written by the FOLD epilogue / embed_ssq) -- the
-  // separate residual_rmsnorm launch disappears
-  const float* nx;
-  const float* nssq;
-  const bf16_t* ng;
-  int nP;
-  float neps;
-  // FOLD epilogue: residual fx[M][N] (+)= slabs, sums of squares fssq[M][N/16], one
-  // arrival counter per column tile (zeroed before the launch)
-  float* fx;
-  float* fssq;
-  unsigned* tickets;
 };
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm)
 bool gemv_split_supported(int M, int N, int K, int S);
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s);
-// split-K with the decode-chain options of ga (NORM prologue: ga->nx; FOLD epilogue: ga->fx)
-void launch_gemv_split_ex(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
-                          const GemvArgs* ga, hipStream_t s);
-// the X image of a NORM prologue must fit LDS (M rows of the block's K range)
-bool gemv_norm_supported(int M, int K);
 // rows of {max, id} partials [rows][tiles] -> ids (-1: no finite maximum)
 void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* out, hipStream_t s);
-// decode embedding: x[t] = E[ids[t]] and ssq[t][c] = sum of squares of columns 16c..16c+15
-void launch_embed_ssq(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, float* ssq,
-                      hipStream_t s);
+
 // x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = RMSNorm(x)*w.
 // S = 0: plain RMSNorm.  Supported: S <= 8, H <= 3072 (H > 3072 only with S = 0).
 bool residual_rmsnorm_supported(int S, int H);
@@ -141,7 +117,7 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 bool qgemv_supported(int M, int N, int K, int epi);
 bool qgemv_split_supported(int M, int N, int K, int S);
 void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
-                        hipStream_t s, const GemvArgs* ga = nullptr);
+                        hipStream_t s);
 void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga, hipStream_t s);
 

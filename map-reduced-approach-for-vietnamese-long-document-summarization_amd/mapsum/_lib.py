@@ -19,6 +19,7 @@ MS_FLAG_IGNORE_EOS = 1
 (MS_T_EMBED, MS_T_ATTN_NORM, MS_T_WQ, MS_T_WK, MS_T_WV, MS_T_WO, MS_T_FFN_NORM, MS_T_WGATE,
  MS_T_WUP, MS_T_WDOWN, MS_T_FINAL_NORM, MS_T_LM_HEAD) = range(12)
 MS_EPI_STORE_BF16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
+MS_EPI_ARGMAX = 5
 MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms
 K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC = range(6)
@@ -29,7 +30,7 @@ EXPORTED = (
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
-    "ms_op_argmax", "ms_set_gemm_variant",
+    "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
 )
 
 
@@ -103,6 +104,7 @@ def load() -> C.CDLL:
         "ms_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, C.c_float, vp, vp]),
         "ms_set_gemm_variant": (i32, [i32]),
         "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
+        "ms_op_argmax_partials": (i32, [vp, i32, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -185,10 +185,9 @@ def test_fullshape_batch_invariance(eng, chunks, batch_out):
 
 
 @pytest.mark.timeout(900)
-def test_fullshape_decode_b32_norm_fallback(oracle, chunks):
-    """B = 32 at the full width: the gate/up projection's RMSNorm image (32 x 3072 bf16) no
-    longer fits LDS, so the chain runs a standalone RMSNorm there; tokens still agree with
-    the oracle (teacher-forced, near-tie rule)."""
+def test_fullshape_decode_b32(oracle, chunks):
+    """B = 32 at the full width (MT = 2 GEMV tiles; the gate/up X image no longer fits LDS
+    and is read from L2): tokens agree with the oracle (teacher-forced, near-tie rule)."""
     e = Engine(CFG, device=0, max_batch=32, max_ctx=256, max_prefill_tokens=4096)
     try:
         e.init_synthetic(SEED, STD, JIT)

@@ -186,6 +186,45 @@ def test_residual_rmsnorm(lib, dev, S):
     assert torch.equal(y, y2), "fused residual+norm must equal the plain norm of the same x"
 
 
+@pytest.mark.parametrize("M", [1, 8, 33])
+def test_lm_head_argmax_epilogue(lib, dev, M):
+    """The decode lm_head's argmax epilogue ({max, id} per 16-column tile) + the partials
+    merge == argmax of the fp32 logits: ties -> lowest id, NaN never wins, a row with no
+    finite logit -> -1 (the engine's per-chunk MS_FINISH_ERROR)."""
+    K, N = 768, 4096
+    g = torch.Generator(device="cpu").manual_seed(M)
+    X = _bf16(torch.randn(M, K, generator=g))
+    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    X[0] = 0.0  # row 0: every logit 0 -> a full tie -> id 0
+    W[1234] = W[77]  # duplicate rows: exact ties between ids 77 and 1234
+    if M > 1:
+        X[1] = W[77].float() * 10  # row 1 prefers 77 (tied with 1234)
+    if M > 2:
+        X[2, 5] = float("nan")  # row 2: NaN everywhere -> -1
+    X, W = X.to(dev), W.to(dev)
+    tiles = N // 16
+    part = torch.empty(M, tiles, 2, dtype=torch.float32, device=dev)
+    ws = torch.zeros(256, dtype=torch.uint8, device=dev)
+    ids = torch.empty(M, dtype=torch.int32, device=dev)
+    L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), part.data_ptr(), M, N, K, tiles, L.MS_EPI_ARGMAX,
+                           ws.data_ptr(), _stream()))
+    L.check(lib.ms_op_argmax_partials(part.data_ptr(), M, tiles, ids.data_ptr(), _stream()))
+    logits = torch.zeros(M, N, dtype=torch.float32, device=dev)
+    L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), logits.data_ptr(), M, N, K, N, L.MS_EPI_STORE_F32,
+                           ws.data_ptr(), _stream()))
+    torch.cuda.synchronize()
+    got = ids.cpu().tolist()
+    lg = logits.cpu()
+    for r in range(M):
+        if M > 2 and r == 2:
+            assert got[r] == -1
+            continue
+        assert got[r] == int(torch.argmax(lg[r])), r  # torch: first occurrence = lowest id
+    assert got[0] == 0
+    if M > 1:
+        assert got[1] == 77
+
+
 def test_rmsnorm_and_argmax(lib, dev):
     g = torch.Generator(device="cpu").manual_seed(5)
     x = (torch.randn(37, 768, generator=g) * 3).to(dev)
@@ -340,13 +379,11 @@ def test_errors_are_reported(dev):
         e.close()
 
 
-@pytest.mark.parametrize("chain,slabs,fused", [(1, 1, 1), (0, 0, 0), (0, 0, 1), (0, 1, 0), (0, 1, 1)])
-def test_decode_attention_variants(oracle, monkeypatch, chain, slabs, fused):
-    """The decode variants -- the chain (RMSNorm in the projections' staging, split-K slabs
-    folded in-launch, attention split combine in-launch, argmax partials in the lm_head
-    epilogue) and the older launch sequences (q/k/v from QKV split slabs or from the GEMV
-    RoPE epilogue; split combine in-launch or as a second launch) -- all agree with the oracle."""
-    monkeypatch.setenv("MS_CHAIN", str(chain))
+@pytest.mark.parametrize("slabs,fused", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
+    """The decode-attention variants (q/k/v from QKV split slabs or from the GEMV RoPE
+    epilogue; split combine in-launch -- write-through partials + arrival counter -- or as a
+    second launch) all agree with the oracle."""
     monkeypatch.setenv("MS_ATTN_SLABS", str(slabs))
     monkeypatch.setenv("MS_ATTN_FUSED_COMBINE", str(fused))
     e = Engine(TINY, device=0, max_batch=6, max_ctx=1024, max_prefill_tokens=4096)
