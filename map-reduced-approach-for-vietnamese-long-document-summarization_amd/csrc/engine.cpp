@@ -901,7 +901,7 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
   PrefillAttnArgs pa{};
   // in-launch split-combine counters start at zero every step (a memset node)
-  HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
+  if (E.attn_fused_combine) HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
   E.prof_begin(K_MISC);
   launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
   E.prof_end(K_MISC);

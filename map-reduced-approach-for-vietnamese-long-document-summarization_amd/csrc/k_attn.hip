@@ -210,7 +210,16 @@ constexpr int kSplitPages = 4;  // = waves per block
 constexpr int kMaxGroup = 8;    // q heads per kv head
 constexpr int kMaxSlabs = 8;    // QKV split-K slabs (engine kMaxSplit)
 
-static int decode_nsplit(int max_len) { return (max_len + kSplitPages * kPage - 1) / (kSplitPages * kPage); }
+// pages per wave: 2 halves the block count (one resident round instead of 1.1 at B = 8,
+// 2304 keys), the second page's loads issued under the first page's math (MS_ATTN_PPW)
+static int decode_ppw() {
+  static const int v = [] { const char* e = getenv("MS_ATTN_PPW"); return e ? atoi(e) : 2; }();
+  return v == 1 ? 1 : 2;
+}
+static int decode_nsplit(int max_len) {
+  const int per = kSplitPages * kPage * decode_ppw();
+  return (max_len + per - 1) / per;
+}
 
 constexpr int kMaxTickets = 4096;  // (b, kv head) pairs per launch
 constexpr int kMaxSplits = 127;
@@ -228,8 +237,8 @@ bool attn_decode_supported(int B, int Hq, int Hk, int max_len) {
          decode_nsplit(max_len) <= kMaxSplits;
 }
 
-template <bool FROM_SLABS, bool FUSED_COMBINE>
-__global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
+template <bool FROM_SLABS, bool FUSED_COMBINE, int PPW>
+__global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
                                                           DecodeAttnArgs a, float* __restrict__ ws,
                                                           unsigned* __restrict__ tickets,
                                                           bf16_t* __restrict__ out, int nsplit,
@@ -243,31 +252,38 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
   const int slot = a.seq_slot[b];
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
   char* vs_ = smem + wave * 16384;
-  const int pg = split * kSplitPages + wave;
-  const bool active = pg * kPage < len;  // wave-uniform
+  // this wave's pages: pp-th = split*4*PPW + pp*4 + wave (interleaved: waves stay balanced)
+  const int pg0 = split * kSplitPages * PPW + wave;
   const int pos = len - 1;               // the new token
   bf16_t* qn = (bf16_t*)(smem + 4 * 16384);  // [G][128] roped q
   bf16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
   bf16_t* vn = kn + kHeadDim;                 // [128] v of the new token
+  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
 
-  // issue the whole page first -- K fragments (16 rows x 64 B per instruction) and V rows
-  // (1 KB) -- so its HBM latency overlaps the q/k/v prologue
+  // K fragments (16 rows x 64 B per instruction) and V rows (1 KB) of one page
   u32x4 kf[4][4], vr[16];
-  if (active) {
-    const size_t base =
-        ((size_t)kv.block_table[(size_t)slot * kv.max_pages + pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  auto fetch_k = [&](int pg) {
+    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
         kf[mt][s4] = *(const u32x4*)(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
+  };
+  auto fetch_v = [&](int pg) {
+    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       vr[i] = *(const u32x4*)(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
+  };
+  // issue the first page first, so its HBM latency overlaps the q/k/v prologue
+  if (pg0 * kPage < len) {
+    fetch_k(pg0);
+    fetch_v(pg0);
   }
 
   if constexpr (FROM_SLABS) {
-    const bool owns_new = (pos / kPage) / kSplitPages == split;  // block-uniform
+    const bool owns_new = (pos / kPage) / (kSplitPages * PPW) == split;  // block-uniform
     float* raw = (float*)smem;  // [(G+2)][128] bf16-rounded sums; aliases wave 0's V image
     const size_t sstride = (size_t)a.B * row_stride;
     const float* src = qa.slabs + (size_t)b * row_stride;
@@ -311,7 +327,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
     if (owns_new && tid < kHeadDim) vn[tid] = f2bf(raw[(G + 1) * kHeadDim + tid]);
     __syncthreads();  // raw consumed (wave 0 may stage V); qn/kn/vn ready
     if (owns_new && tid < kHeadDim) {  // the new token's K/V into the cache, for later steps
-      const int page = kv.block_table[(size_t)slot * kv.max_pages + pos / kPage];
+      const int page = bt[pos / kPage];
       const size_t o = (((size_t)page * kv.n_kv_heads + kvh) * kPage + pos % kPage) * kHeadDim + tid;
       kv.k[o] = kn[tid];
       kv.v[o] = vn[tid];
@@ -323,7 +339,7 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  if (active) {
+  if (pg0 * kPage < len) {
     bf16x8 qf[4];
     {
       const int hl = min(r, G - 1);
@@ -336,65 +352,77 @@ __global__ __launch_bounds__(256) void attn_decode_kernel(DecodeQKV qa, int Hq, 
         for (int s4 = 0; s4 < 4; ++s4) qf[s4] = as_bf16x8(*(const uint4*)(qrow + 32 * s4 + 8 * g));
       }
     }
-    const bool patch = FROM_SLABS && pg == pos / kPage;  // wave-uniform: holds the new token
     const int off = pos % kPage;
-    if (patch) {
+#pragma unroll
+    for (int pp = 0; pp < PPW; ++pp) {
+      const int pg = pg0 + pp * kSplitPages;
+      if (pg * kPage >= len) break;  // wave-uniform
+      const bool more = pp + 1 < PPW && (pg + kSplitPages) * kPage < len;
+      const bool patch = FROM_SLABS && pg == pos / kPage;  // wave-uniform: holds the new token
+      if (patch) {
+#pragma unroll
+        for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+          for (int s4 = 0; s4 < 4; ++s4)
+            if (mt * 16 + r == off) kf[mt][s4] = *(const u32x4*)(kn + 32 * s4 + 8 * g);
+      }
+      f32x4 sc[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) {
+        sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
+      }
+      if (more) fetch_k(pg + kSplitPages);  // K registers are free: next page's K in flight
+      float mx = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4)
-          if (mt * 16 + r == off) kf[mt][s4] = *(const u32x4*)(kn + 32 * s4 + 8 * g);
-    }
-    f32x4 sc[4];
+        for (int j = 0; j < 4; ++j) {
+          const int key = pg * kPage + mt * 16 + 4 * g + j;
+          const float v = (key >= len) ? -INFINITY : sc[mt][j] * scale_log2;
+          sc[mt][j] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);  // finite: key pg*64 < len is always visible
+      const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
+      float rs = 0.f;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
-      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
-    }
-    float mx = -INFINITY;
+        for (int j = 0; j < 4; ++j) {
+          const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - m_new);
+          sc[mt][j] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+      // V rows -> this wave's LDS image (rows past len zeroed: no stale V in P.V)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = pg * kPage + mt * 16 + 4 * g + j;
-        const float v = (key >= len) ? -INFINITY : sc[mt][j] * scale_log2;
-        sc[mt][j] = v;
-        mx = fmaxf(mx, v);
+      for (int i = 0; i < 16; ++i) {
+        const int row = i * 4 + (lane >> 4);
+        if (pg * kPage + row >= len) vr[i] = u32x4{0, 0, 0, 0};
+        if (patch && row == off) vr[i] = *(const u32x4*)(vn + (lane & 15) * 8);
+        *(u32x4*)(vs_ + v_swz(row, lane & 15)) = vr[i];
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    m_run = mx;  // finite: key pg*64 < len is always visible
-    float rs = 0.f;
+      if (more) fetch_v(pg + kSplitPages);  // V registers are free: next page's V in flight
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the V image is in LDS
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int kstep = 0; kstep < 2; ++kstep) {
+        const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - mx);
-        sc[mt][j] = p;
-        rs += p;
+        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
       }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l_run = rs;
-    // V rows -> this wave's LDS image (rows past len zeroed: no stale V in P.V)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int row = i * 4 + (lane >> 4);
-      if (pg * kPage + row >= len) vr[i] = u32x4{0, 0, 0, 0};
-      if (patch && row == off) vr[i] = *(const u32x4*)(vn + (lane & 15) * 8);
-      *(u32x4*)(vs_ + v_swz(row, lane & 15)) = vr[i];
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the V image is in LDS
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int kstep = 0; kstep < 2; ++kstep) {
-      const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_wave_barrier();
   }
   // publish (m, l, O^T) of this wave's 16 columns into its own LDS region
   {
@@ -531,9 +559,15 @@ void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView
   unsigned* tickets = (unsigned*)ws;
   ws = (float*)((char*)ws + (size_t)kMaxTickets * 4);
   const dim3 grid(a.B, Hk, nsplit);
-#define AD(SL, FC)                                                                                   \
-  MS_LAUNCH((attn_decode_kernel<SL, FC>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
-            nsplit, scale_log2)
+#define AD(SL, FC)                                                                                        \
+  do {                                                                                                     \
+    if (decode_ppw() == 2)                                                                                 \
+      MS_LAUNCH((attn_decode_kernel<SL, FC, 2>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
+                nsplit, scale_log2);                                                                       \
+    else                                                                                                   \
+      MS_LAUNCH((attn_decode_kernel<SL, FC, 1>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
+                nsplit, scale_log2);                                                                       \
+  } while (0)
   if (qa.slabs && fused_combine) AD(true, true);
   else if (qa.slabs) AD(true, false);
   else if (fused_combine) AD(false, true);

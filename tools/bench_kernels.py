@@ -72,13 +72,16 @@ def bench_split(lib, M):
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     for name, N, K in [("o", 3072, 3072), ("down", 3072, 8192), ("qkv", 5120, 3072)]:
-        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02 for _ in range(8)]
+        # enough weight copies that the rotation streams > 512 MB: the 256 MB MALL never
+        # holds the matrix a launch reads (as in a decode step, which streams 6.4 GB)
+        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02
+              for _ in range(max(8, -(-512 * 2**20 // (N * K * 2))))]
         X = torch.randn(M, K, device=dev).to(torch.bfloat16)
         slabs = torch.zeros(8, M, N, device=dev)
         for S in (1, 2, 3, 4, 6, 8):
             byts = N * K * 2 + M * K * 2 + S * M * N * 4
             line = f"{name:5s} N={N:5d} K={K:5d} M={M:2d} S={S} |"
-            for wv in (0, 2, 4, 8, 12, 16):
+            for wv in (0, 1, 2, 3, 4, 6, 8, 12, 16):
                 i = [0]
 
                 def fn():
