@@ -181,6 +181,11 @@ int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, in
 /* tuning hook: as ms_op_gemv with the K-splitting wave count forced (0 = heuristic) */
 int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                      int32_t ldo, int32_t epilogue, void* workspace, int32_t waves, void* stream);
+/* large-batch decode GEMM (M <= 256 rows; 64 weight rows per block, X shared via LDS): the
+   ms_op_gemv epilogues (plus MS_EPI_ARGMAX); S > 1: split-K fp32 slabs [S][M][N] with
+   epilogue MS_EPI_STORE_F32; N % 64 == 0, K % (64 S) == 0 */
+int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
+                int32_t ldo, int32_t epilogue, void* stream);
 /* decode split-K: slabs fp32 [S][M][N], slab s = X[:, sK/S:(s+1)K/S] . W[:, same]^T;
    waves = 0 picks the heuristic (tuning hook otherwise) */
 int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,

@@ -1181,6 +1181,16 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
   });
 }
 
+int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
+                int32_t ldo, int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && W && out, MS_EINVAL, "bad dgemm operands");
+    REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && dgemm_supported(M, N, K, S, epi), MS_EINVAL,
+            "dgemm shape unsupported (M <= 256, N % 64 == 0, K % (64 S) == 0, S > 1 only for fp32 slabs)");
+    launch_dgemm((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, (hipStream_t)stream);
+  });
+}
+
 int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
                      int32_t S, int32_t waves, void* stream) {
   return op_guard([&] {

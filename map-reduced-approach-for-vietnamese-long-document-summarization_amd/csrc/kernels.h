@@ -87,6 +87,13 @@ void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int 
 void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, const GemvArgs* ga, int force_waves, hipStream_t s);
 
+// large-batch decode projections (k_dgemm.hip): 64 weight rows x all M <= 256 rows per block,
+// X shared through LDS; S > 1 = split-K fp32 slabs [S][M][N] (STORE_F32 only).  Epilogues as
+// the GEMV's except ROPE_KV; N % 64 == 0, K % (64 S) == 0.
+bool dgemm_supported(int M, int N, int K, int S, int epi);
+void launch_dgemm(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+                  hipStream_t s);
+
 // ---- ggml K-quant weights (k_qgemv.hip)
 enum { MS_QT_Q4_K = 12, MS_QT_Q6_K = 14 };  // ggml_type ids
 constexpr int kQ4KBytes = 144, kQ6KBytes = 210, kQ6KPacked = 224;

@@ -29,7 +29,7 @@ EXPORTED = (
     "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv", "ms_op_qgemv_split",
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
-    "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
+    "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_dgemm", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
 )
 
@@ -100,6 +100,7 @@ def load() -> C.CDLL:
         "ms_op_gemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),
         "ms_op_gemv_tuned": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp]),
         "ms_op_gemv_split": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
+        "ms_op_dgemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
         "ms_op_residual_rmsnorm": (i32, [vp, vp, i32, vp, vp, i32, i32, C.c_float, vp]),
         "ms_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, C.c_float, vp, vp]),
         "ms_set_gemm_variant": (i32, [i32]),

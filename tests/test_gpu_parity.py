@@ -140,6 +140,54 @@ def test_gemv_vs_torch(lib, dev, M, N, K, epi):
             assert torch.equal(first, o), "gemv must be deterministic"
 
 
+@pytest.mark.parametrize("M", [1, 17, 64, 100, 256])
+@pytest.mark.parametrize("N,K,S,epi", [(1024, 768, 1, L.MS_EPI_STORE_BF16), (768, 2048, 1, L.MS_EPI_ADD_F32),
+                                       (2048, 768, 1, L.MS_EPI_SWIGLU), (3072, 8192, 4, L.MS_EPI_STORE_F32),
+                                       (5120, 3072, 6, L.MS_EPI_STORE_F32), (4096, 768, 1, L.MS_EPI_ARGMAX)])
+def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
+    """The large-batch decode GEMM (k_dgemm.hip) against a float64 reference: fp32 outputs
+    differ only by summation order; split-K slabs are the exact partial products; the
+    argmax partials merge to the fp32 logits' argmax."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + S + epi)
+    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
+    W = _bf16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    ref = X.double().cpu() @ W.double().cpu().T
+    if epi == L.MS_EPI_STORE_F32:
+        out = torch.full((S, M, N), float("nan"), device=dev)
+        L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, S, N, epi, _stream()))
+        torch.cuda.synchronize()
+        ks = K // S
+        for s_ in range(S):
+            exp = X.double().cpu()[:, s_ * ks:(s_ + 1) * ks] @ W.double().cpu()[:, s_ * ks:(s_ + 1) * ks].T
+            assert rel(out[s_].double().cpu(), exp) < 2e-6, s_
+        return
+    if epi == L.MS_EPI_ARGMAX:
+        part = torch.empty(M, N // 16, 2, device=dev)
+        ids = torch.empty(M, dtype=torch.int32, device=dev)
+        L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), part.data_ptr(), M, N, K, 1, N // 16, epi, _stream()))
+        L.check(lib.ms_op_argmax_partials(part.data_ptr(), M, N // 16, ids.data_ptr(), _stream()))
+        torch.cuda.synchronize()
+        srt = torch.sort(ref, 1).values
+        got = ids.cpu().long()
+        for r in range(M):  # the fp64 argmax, unless the top two are within fp32 noise
+            if srt[r, -1] - srt[r, -2] > 1e-4:
+                assert int(got[r]) == int(torch.argmax(ref[r])), r
+        return
+    if epi == L.MS_EPI_SWIGLU:
+        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        r = ref.view(M, N // 32, 2, 16)
+        exp, ldo, tol = (torch.nn.functional.silu(r[:, :, 0]) * r[:, :, 1]).reshape(M, N // 2), N // 2, 4e-3
+    elif epi == L.MS_EPI_STORE_BF16:
+        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+        exp, ldo, tol = ref, N, 4e-3
+    else:
+        out = torch.randn(M, N, generator=g).to(dev)
+        exp, ldo, tol = out.double().cpu() + ref, N, 2e-6
+    L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, S, ldo, epi, _stream()))
+    torch.cuda.synchronize()
+    assert rel(out.double().cpu(), exp) < tol
+
+
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("N,K,S", [(3072, 3072, 4), (3072, 8192, 4), (768, 2048, 2), (256, 768, 3),
                                    (3072, 8192, 8)])

@@ -98,6 +98,50 @@ def bench_split(lib, M):
             print(line, flush=True)
 
 
+def bench_dgemm(lib):
+    """Decode projections over the batch sizes of the continuous batch: the weight-streaming
+    GEMV (M <= 64), the large-batch skinny GEMM (k_dgemm.hip) over split counts, and the
+    prefill GEMM fallback, all on >512 MB weight rotations (no MALL reuse)."""
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    ws = torch.zeros(4096, dtype=torch.uint8, device=dev)
+    for name, N, K, epi, splits in [("qkv", 5120, 3072, 3, (1, 2, 3, 6)), ("o", 3072, 3072, 3, (1, 2, 4, 6)),
+                                    ("gu", 16384, 3072, 2, (1,)), ("down", 3072, 8192, 3, (1, 2, 4, 8)),
+                                    ("lm_head", 128256, 3072, 5, (1,))]:
+        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02
+              for _ in range(max(2, -(-512 * 2**20 // (N * K * 2))))]
+        for M in (8, 16, 32, 64, 128, 256):
+            X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            out = torch.zeros(8 * M * N, device=dev)
+            wbytes = N * K * 2
+            line = f"{name:7s} N={N:6d} K={K:5d} M={M:3d} |"
+            i = [0]
+
+            def nextw():
+                i[0] += 1
+                return Ws[i[0] % len(Ws)]
+            ldo = N // 2 if epi == 2 else (N // 16 if epi == 5 else N)
+            if M <= 64:
+                t = timeit(lambda: lib.ms_op_gemv(X.data_ptr(), nextw().data_ptr(), out.data_ptr(), M, N, K, ldo,
+                                                  epi, ws.data_ptr(), st))
+                line += f" gemv {t*1e3:6.1f}us {wbytes/t/1e6:5.0f} |"
+            for S in splits:
+                e = epi if S == 1 else 3
+                rc = lib.ms_op_dgemm(X.data_ptr(), Ws[0].data_ptr(), out.data_ptr(), M, N, K, S, ldo if S == 1 else N,
+                                     e, st)
+                if rc:
+                    line += f" dg S{S} n/a |"
+                    continue
+                t = timeit(lambda: lib.ms_op_dgemm(X.data_ptr(), nextw().data_ptr(), out.data_ptr(), M, N, K, S,
+                                                   ldo if S == 1 else N, e, st))
+                line += f" dg S{S} {t*1e3:6.1f}us {wbytes/t/1e6:5.0f} |"
+            if M > 16 and epi != 5:
+                e = epi if epi != 5 else 3
+                t = timeit(lambda: lib.ms_op_gemm(X.data_ptr(), nextw().data_ptr(), out.data_ptr(), M, N, K, ldo, e, st))
+                line += f" gemm {t*1e3:6.1f}us |"
+            print(line, flush=True)
+
+
 def bench_gemm(lib):
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -122,7 +166,7 @@ def bench_gemm(lib):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm", "split"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm"])
     ap.add_argument("--m", type=int, default=8)
     a = ap.parse_args()
     lib = L.load()
@@ -132,5 +176,7 @@ if __name__ == "__main__":
         bench_gemv(lib, a.m, shapes, [0, 6, 8, 12, 16])
     elif a.what == "split":
         bench_split(lib, a.m)
+    elif a.what == "dgemm":
+        bench_dgemm(lib)
     else:
         bench_gemm(lib)
