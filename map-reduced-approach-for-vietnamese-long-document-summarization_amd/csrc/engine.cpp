@@ -111,6 +111,12 @@ struct ms_engine {
   // residual by the next residual_rmsnorm launch (pending_split = S of the unfolded slabs)
   float* slabs = nullptr;
   int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
+  // large-batch regime (B >= dgemm_min rows in flight, BASELINE configs[2]): QKV / O / down /
+  // lm_head on the skinny GEMM (k_dgemm.hip, split 6 / 6 / 8 / 1), gate/up on the 128x128
+  // GEMM.  Each regime is batch-invariant on its own (no kernel choice inside it depends on
+  // B); between the regimes a row's summation order differs.
+  int dgemm_min = 49, dsplit_qkv = 6, dsplit_o = 6, dsplit_down = 8;
+  bool large(int B) const { return B >= dgemm_min; }
   int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
   // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
@@ -212,18 +218,27 @@ struct ms_engine {
   // decode with fused epilogues: residual+norm, QKV+RoPE+KV-scatter, attention(+combine),
   // O (split-K slabs), residual+norm, gate/up+SwiGLU, down (split-K slabs)
   bool fused_decode(int B) const {
-    return B <= kMaxSlabRows && residual_rmsnorm_supported(kMaxSplit, H) &&
+    if (large(B))
+      return B <= kMaxSlabRows && attn_slabs && residual_rmsnorm_supported(kMaxSplit, H) &&
+             dgemm_supported(B, QKVN, H, dsplit_qkv, MS_GEMV_EPI_STORE_F32) &&
+             dgemm_supported(B, H, Hq * D, dsplit_o, MS_GEMV_EPI_STORE_F32) &&
+             dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32) && (2 * F) % 32 == 0 &&
+             attn_decode_supported(B, Hq, Hk, max_pages * kPage);
+    return B <= kMaxGemvRows && residual_rmsnorm_supported(kMaxSplit, H) &&
            (attn_slabs ? gemv_split_supported(B, QKVN, H, 1) : gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
            gemv_split_supported(B, H, Hq * D, 1) && gemv_split_supported(B, H, F, 1) &&
            attn_decode_supported(B, Hq, Hk, max_pages * kPage);
   }
-  static constexpr int kMaxSlabRows = 64, kMaxSplit = 8;
+  static constexpr int kMaxGemvRows = 64, kMaxSlabRows = 256, kMaxSplit = 8;
 
   // projection into fp32 partial slabs [S][M][N]; returns the number of slabs written
-  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S) {
+  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int Sl) {
     prof_begin(K_GEMV);
     int used = 1;
-    if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
+    if (large(M)) {  // skinny GEMM on the bf16 weights (K-quant copies included)
+      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream);
+      used = Sl;
+    } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
       // Q4_K/Q6_K: same split-K as bf16 (a 16-row tile carries 3.6x fewer weight bytes, so
       // the unsplit grid -- 192 blocks for O/down -- is too thin to cover 256 CUs)
       const int Sq = qsplit > 0 ? qsplit : S;
@@ -259,7 +274,7 @@ struct ms_engine {
     DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab};
     if (attn_slabs) {
       // QKV -> slabs; attention adds them, applies RoPE and writes the new K/V (k_attn.hip)
-      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv);
+      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv, dsplit_qkv);
     } else {
       // QKV GEMV epilogue: RoPE, q -> qkv rows, K/V -> paged cache
       GemvArgs ga{};
@@ -276,10 +291,16 @@ struct ms_engine {
     prof_begin(K_ATTN_DECODE);
     launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
     prof_end(K_ATTN_DECODE);
-    pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o);
+    pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
     residual_norm(Ly.ffn_norm, B);
-    proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
-    pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down);
+    if (large(B)) {
+      prof_begin(K_GEMV);
+      launch_gemm(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_EPI_SWIGLU, stream);
+      prof_end(K_GEMV);
+    } else {
+      proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
+    }
+    pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down, dsplit_down);
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
@@ -469,12 +490,14 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.gemv_ws = E.dalloc<char>(gws, true);
     E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
                                        true);  // zeroed: split-combine tickets
-    E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * ms_engine::kMaxSlabRows * std::max(E.QKVN, E.H));
+    E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * std::min(std::max(cfg->max_batch, 64), 256) *
+                              std::max(E.QKVN, E.H));
     if (const char* v = getenv("MS_SPLIT_QKV")) E.split_qkv = atoi(v);
     if (const char* v = getenv("MS_ATTN_SLABS")) E.attn_slabs = atoi(v) != 0;
     if (const char* v = getenv("MS_ATTN_FUSED_COMBINE")) E.attn_fused_combine = atoi(v) != 0;
     if (const char* v = getenv("MS_SPLIT_O")) E.split_o = atoi(v);
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
+    if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
@@ -883,8 +906,8 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   E.prof_end(K_MISC);
   // the first token goes through the decode lm_head GEMV in row groups of <= 64: its sum
   // order is then the decode steps' one whatever the number of admitted prompts
-  for (int r0 = 0; r0 < S; r0 += ms_engine::kMaxSlabRows) {
-    const int rows = std::min(S - r0, (int)ms_engine::kMaxSlabRows);
+  for (int r0 = 0; r0 < S; r0 += ms_engine::kMaxGemvRows) {
+    const int rows = std::min(S - r0, (int)ms_engine::kMaxGemvRows);
     E.gemm_or_gemv(E.xb + (size_t)r0 * E.H, E.lm_head, E.logits + (size_t)r0 * E.V, rows, E.V, E.H, E.V,
                    MS_EPI_STORE_F32, true, K_LMHEAD);
   }
@@ -908,7 +931,15 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   E.pending_split = 0;
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   E.residual_norm(E.final_norm, B);  // folds the last layer's down slabs (if fused)
-  if (gemv_supported(B, E.V, E.H, MS_GEMV_EPI_ARGMAX)) {
+  if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX)) {
+    const int tiles = E.V / 16;
+    E.prof_begin(K_LMHEAD);
+    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream);
+    E.prof_end(K_LMHEAD);
+    E.prof_begin(K_MISC);
+    launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
+    E.prof_end(K_MISC);
+  } else if (gemv_supported(B, E.V, E.H, MS_GEMV_EPI_ARGMAX)) {
     // greedy argmax in the lm_head epilogue: {max, id} per 16-column tile, no logits row
     const int tiles = E.V / 16;
     E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, nullptr, K_LMHEAD);

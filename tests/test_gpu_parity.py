@@ -384,6 +384,20 @@ def test_batch_invariance(eng):
         assert alone.ids == r.ids
 
 
+def test_batch_invariance_large_regime(dev):
+    """Within the large-batch regime (B >= 49 rows in flight) a chunk's summary does not
+    depend on its companions either: the first 60 of 100 chunks alone == in the batch."""
+    e = Engine(TINY, device=0, max_batch=100, max_ctx=256, max_prefill_tokens=16384)
+    try:
+        e.init_synthetic(SEED, STD, JITTER)
+        prompts = [_prompt(20 + (11 * i) % 100, 1300 + i) for i in range(100)]
+        together = e.generate(prompts, num_predict=10, ignore_eos=True)
+        alone = e.generate(prompts[:60], num_predict=10, ignore_eos=True)
+        assert [r.ids for r in alone] == [r.ids for r in together[:60]]
+    finally:
+        e.close()
+
+
 def test_eos_stops_and_is_dropped(dev, oracle):
     """With the oracle's own first greedy token declared EOS the chunk ends at once,
     empty -- as Ollama drops <|eot_id|> from `response`."""
@@ -454,11 +468,12 @@ def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
         e.close()
 
 
-@pytest.mark.parametrize("nb", [20, 70])
+@pytest.mark.parametrize("nb", [20, 50, 70, 130])
 def test_decode_paths_larger_batch(oracle, nb):
-    """B = 20 runs the fused decode chain with MT = 2 GEMV tiles; B = 70 > 64 the unfused
-    chain (RMSNorm kernel, prefill GEMM, RoPE kernel, attention on roped bf16 q).  Both
-    must agree with the oracle (teacher-forced, flips only at near-ties)."""
+    """B = 20 runs the weight-streaming GEMVs with MT = 2 tiles; B >= 49 the large-batch
+    regime (skinny GEMM k_dgemm.hip for QKV / O / down / lm_head with split-K slabs, the
+    128x128 GEMM for gate/up).  All must agree with the oracle (teacher-forced, flips only
+    at near-ties)."""
     e = Engine(TINY, device=0, max_batch=nb, max_ctx=256, max_prefill_tokens=8192)
     try:
         e.init_synthetic(SEED, STD, JITTER)
