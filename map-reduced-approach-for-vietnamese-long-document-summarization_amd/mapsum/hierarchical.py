@@ -119,7 +119,11 @@ class RecursiveCharacterTextSplitter:
                 sep, rest = s, separators[i + 1:]
                 break
         good = []
-        for piece in self._split_keep(text, sep):
+        pieces = self._split_keep(text, sep)
+        prime = getattr(self.length, "prime", None)
+        if prime is not None:  # a batched length function measures every piece in one call
+            prime(pieces + [""])
+        for piece in pieces:
             if self.length(piece) < self.chunk_size:
                 good.append(piece)
                 continue

@@ -111,3 +111,13 @@ def run_map_reduce(llm, contents: list, token_max: int = 1000, recursion_limit: 
                    map_prompt=None) -> MapReduceTrace:
     """Synchronous entry (a fresh event loop), like ``asyncio.run(summarize_document_mapreduce)``."""
     return asyncio.run(arun_map_reduce(llm, contents, token_max, recursion_limit, map_prompt))
+
+
+async def asummarize_document_mapreduce(doc_text: str, llm, text_splitter, token_max: int = 1000,
+                                        recursion_limit: int = 10) -> str:
+    """summarize_document_mapreduce (runners/run_summarization_ollama_mapreduce.py:183-201):
+    split the document (``text_splitter.split_documents`` of one Document == split_text of
+    its text), then the map-reduce graph; returns the final summary."""
+    contents = text_splitter.split_text(doc_text)
+    tr = await arun_map_reduce(llm, contents, token_max=token_max, recursion_limit=recursion_limit)
+    return tr.final_summary
