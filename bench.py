@@ -170,6 +170,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip HIP-event timing of the GEMV class")
     ap.add_argument("--no-check", action="store_true", help="skip the output self-checks")
+    ap.add_argument("--bcast-weights", action="store_true",
+                    help="N > 1: rank 0 makes the weights, the other ranks receive them over RCCL")
     return ap.parse_args(argv)
 
 
@@ -211,10 +213,17 @@ def main():
     eng = Engine(cfg, device=local_rank, max_batch=B, max_ctx=max_ctx,
                  max_prefill_tokens=min(B, 8) * args.prompt_len)
     quant = args.weights == "q4_k_m"
-    if quant:
-        eng.init_synthetic_q(seed=2, scale=0.02, norm_jitter=0.0)
-    else:
-        eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
+    t_load = time.perf_counter()
+    if rank == 0 or not (args.bcast_weights and world > 1):
+        if quant:
+            eng.init_synthetic_q(seed=2, scale=0.02, norm_jitter=0.0)
+        else:
+            eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
+    bcast_bytes = 0
+    if args.bcast_weights and world > 1:
+        from mapsum.dist import broadcast_engine_weights
+        bcast_bytes = broadcast_engine_weights(eng, src=0)
+    t_load = time.perf_counter() - t_load
     chunks = [synthetic_chunks(1, args.prompt_len, u.doc, cfg.vocab, cfg.bos_id, first_chunk=u.chunk)[0]
               for u in units]
     gather_s = [0.0]
@@ -329,6 +338,8 @@ def main():
                       "decode_steps": st["decode_steps"],
                       "decode_ms_per_decode_step": round(st["decode_ms"] / max(st["decode_steps"], 1), 4),
                       "gather_ms_per_step": round(gather_s[0] / args.steps * 1e3, 3),
+                      "weight_load_s": round(t_load, 3),
+                      "weight_bcast_bytes": bcast_bytes,
                       "prefill_tflops": round(pre_tf, 1) if pre_tf else None},
         "roofline": roof,
         "roofline_prefill": roof_pre,

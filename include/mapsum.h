@@ -140,6 +140,16 @@ int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggml_t
 /* random Q4_K/Q6_K blocks with the Q4_K_M per-tensor type mix (bench) */
 int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float norm_jitter);
 
+/* ---- weight broadcast (one process per GPU: rank 0 loads, the others receive over RCCL) -- */
+/* every device weight buffer in a fixed order (bf16 matrices and norms, then K-quant
+   regions); returns the count, fills up to cap (ptr, bytes) pairs */
+int ms_weight_regions(const ms_engine* e, void** ptrs, int64_t* bytes, int32_t cap);
+/* the (tensor, layer, ggml_type) triples of the K-quant tensors loaded so far; returns the count */
+int ms_quant_manifest(const ms_engine* e, int32_t* triples, int32_t cap);
+/* lay out a K-quant tensor as ms_load_weight_q would, without its bytes (a broadcast fills
+   the regions afterwards) */
+int ms_declare_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggml_type);
+
 /* ---- request path (replaces one /api/generate per chunk) -------------------- */
 int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict,
               uint32_t flags, uint64_t tag);

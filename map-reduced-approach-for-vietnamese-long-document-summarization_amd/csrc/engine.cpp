@@ -77,6 +77,7 @@ struct Layer {
 // logical tensors that must all be loaded quantised before decode uses it.
 struct QSlot {
   QMat m{};
+  size_t bytes[3] = {0, 0, 0};  // device bytes of each region (weight broadcast)
   uint32_t loaded = 0, need = 0;
   bool ready() const { return need != 0 && loaded == need; }
 };
@@ -335,6 +336,41 @@ struct ms_engine {
     prof_end(K_MISC);
     gemm_or_gemv(xb, Ly.wgu, hbuf, T, 2 * F, H, F, MS_EPI_SWIGLU, decode, kc);
     gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
+  }
+
+  // K-quant tensors loaded so far, (tensor, layer, ggml type) in load order: the manifest a
+  // weight broadcast replays on the receiving ranks (ms_quant_manifest / ms_declare_weight_q)
+  std::vector<std::array<int32_t, 3>> quant_manifest;
+  void note_quant(int tensor, int layer, int type) {
+    for (auto& q : quant_manifest)
+      if (q[0] == tensor && q[1] == layer) { q[2] = type; return; }
+    quant_manifest.push_back({tensor, layer, type});
+  }
+  // every device weight buffer, in a fixed order: bf16 matrices and norms, then the K-quant
+  // regions (the payload of a weight broadcast, dist.broadcast_engine_weights)
+  std::vector<std::pair<void*, size_t>> weight_regions() const {
+    std::vector<std::pair<void*, size_t>> r;
+    const size_t H2 = (size_t)H * 2;
+    r.push_back({embed, (size_t)V * H2});
+    if (!cfg.tie_embeddings) r.push_back({lm_head, (size_t)V * H2});
+    r.push_back({final_norm, H2});
+    for (const Layer& Ly : layers) {
+      r.push_back({Ly.attn_norm, H2});
+      r.push_back({Ly.ffn_norm, H2});
+      r.push_back({Ly.wqkv, (size_t)QKVN * H2});
+      r.push_back({Ly.wo, (size_t)Hq * D * H2});
+      r.push_back({Ly.wgu, (size_t)2 * F * H2});
+      r.push_back({Ly.wdown, (size_t)F * H2});
+    }
+    auto qs = [&](const QSlot& q) {
+      const uint8_t* b[3] = {q.m.base0, q.m.base1, q.m.base2};
+      for (int i = 0; i < 3; ++i)
+        if (b[i]) r.push_back({(void*)b[i], q.bytes[i]});
+    };
+    qs(lmq);
+    for (const auto& l : lq)
+      for (const QSlot& q : l) qs(q);
+    return r;
   }
 
   // Captured decode graphs bake in the weight form (bf16 vs K-quant stream) and the split
@@ -631,6 +667,7 @@ static uint8_t* q_region(ms_engine& E, QSlot& s, int idx, int row0, int rows, in
   const int rowb = (K / 256) * qblock_bytes(type, true);
   uint8_t* p = E.dalloc<uint8_t>((size_t)rows * rowb);
   *base = p; *rw0 = row0; *ty = type; *rb = rowb;
+  s.bytes[idx] = (size_t)rows * rowb;
   s.m.n = std::max(s.m.n, idx + 1);
   return p;
 }
@@ -648,6 +685,7 @@ static void load_quant(ms_engine& E, int tensor, int layer, int type, const uint
     t.qs->loaded |= (uint32_t)t.qbit;
     t.qs->need = (uint32_t)t.qneed;
   }
+  E.note_quant(tensor, layer, type);
 }
 
 int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t type, const void* host,
@@ -677,6 +715,43 @@ int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t type, 
     (void)hipFree(tmp);
     return rc;
   });
+}
+
+int ms_declare_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t type) {
+  if (!e) return MS_EINVAL;
+  e->drop_graphs();
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K (12) or Q6_K (14)");
+    HIP_OK(hipSetDevice(E.cfg.device));
+    TensorDst t = tensor_dst(E, tensor, layer);
+    REQUIRE(t.rows > 1 && t.cols % 256 == 0, MS_EINVAL, "not a K-quant matrix");
+    if (t.qs) {  // the layout of a quantised load, without its bytes (a broadcast fills them)
+      q_region(E, *t.qs, t.qregion, t.qrow0, t.qrows, type, t.cols);
+      t.qs->loaded |= (uint32_t)t.qbit;
+      t.qs->need = (uint32_t)t.qneed;
+    }
+    E.note_quant(tensor, layer, type);
+    return MS_OK;
+  });
+}
+
+int ms_quant_manifest(const ms_engine* e, int32_t* triples, int32_t cap) {
+  if (!e || cap < 0 || (cap > 0 && !triples)) return MS_EINVAL;
+  const int n = (int)e->quant_manifest.size();
+  for (int i = 0; i < std::min(n, (int)cap); ++i)
+    for (int j = 0; j < 3; ++j) triples[3 * i + j] = e->quant_manifest[i][j];
+  return n;
+}
+
+int ms_weight_regions(const ms_engine* e, void** ptrs, int64_t* bytes, int32_t cap) {
+  if (!e || cap < 0 || (cap > 0 && (!ptrs || !bytes))) return MS_EINVAL;
+  const auto r = e->weight_regions();
+  for (int i = 0; i < std::min((int)r.size(), (int)cap); ++i) {
+    ptrs[i] = r[i].first;
+    bytes[i] = (int64_t)r[i].second;
+  }
+  return (int)r.size();
 }
 
 // Q4_K_M per-tensor mix (EXT llama.cpp; restated in oracle/quants.py q4_k_m_type)

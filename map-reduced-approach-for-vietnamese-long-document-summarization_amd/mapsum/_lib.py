@@ -31,6 +31,7 @@ EXPORTED = (
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_dgemm", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
+    "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
 )
 
 
@@ -106,6 +107,9 @@ def load() -> C.CDLL:
         "ms_set_gemm_variant": (i32, [i32]),
         "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
         "ms_op_argmax_partials": (i32, [vp, i32, i32, vp, vp]),
+        "ms_weight_regions": (i32, [vp, C.POINTER(vp), C.POINTER(i64), i32]),
+        "ms_quant_manifest": (i32, [vp, pi32, i32]),
+        "ms_declare_weight_q": (i32, [vp, i32, i32, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

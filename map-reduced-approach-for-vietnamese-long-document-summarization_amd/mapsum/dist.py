@@ -84,3 +84,53 @@ def env_rank() -> tuple[int, int, int]:
     """(rank, local_rank, world) from torchrun's environment (1 process if unset)."""
     return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
             int(os.environ.get("WORLD_SIZE", 1)))
+
+
+# ---------------------------------------------------------------- weight broadcast
+class _DeviceBytes:
+    """A zero-copy torch view of engine-owned device memory (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3}
+
+
+def broadcast_tensors(tensors: list, src: int = 0, group=None) -> None:
+    """Broadcast each tensor from ``src`` in place (RCCL over xGMI for CUDA tensors; gloo
+    for the CPU tests)."""
+    import torch.distributed as dist
+    for t in tensors:
+        dist.broadcast(t, src=src, group=group)
+
+
+def broadcast_engine_weights(engine, src: int = 0, group=None) -> int:
+    """SURVEY.md §5 "distributed communication backend": rank ``src`` has loaded the weights
+    (bf16, or a K-quant model); every other rank receives them over RCCL instead of reading
+    the checkpoint itself.  The K-quant layout travels first (a manifest of (tensor, layer,
+    type) the receivers declare), then every device weight buffer, in the engine's fixed
+    region order.  Returns the bytes broadcast."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    box = [engine.quant_manifest() if rank == src else None]
+    dist.broadcast_object_list(box, src=src, group=group)
+    if rank != src:
+        for tensor, layer, ty in box[0]:
+            engine.declare_weight_q(tensor, layer, ty)
+    views = region_views(engine)
+    if views and views[0].is_cuda:
+        torch.cuda.synchronize(views[0].device)
+    broadcast_tensors(views, src=src, group=group)
+    if views and views[0].is_cuda:
+        torch.cuda.synchronize(views[0].device)
+    return sum(v.numel() for v in views)
+
+
+def region_views(engine) -> list:
+    """uint8 tensors aliasing the engine's weight regions (engines that are not libmapsum --
+    the CPU test double -- provide ``region_views`` themselves)."""
+    import torch
+    if hasattr(engine, "region_views"):
+        return engine.region_views()
+    dev = torch.device("cuda", engine.device)
+    return [torch.as_tensor(_DeviceBytes(p, n), device=dev) for p, n in engine.weight_regions()]

@@ -113,6 +113,7 @@ class Engine(RequestQueue):
         L.check(self.lib.ms_create(C.byref(c), C.byref(h)), None, "ms_create")
         self.h = h
         self.max_batch, self.max_ctx, self.max_prefill_tokens = max_batch, max_ctx, max_prefill_tokens
+        self.device = device
         self._next_tag = 1
         self._mailbox = {}
 
@@ -149,6 +150,22 @@ class Engine(RequestQueue):
         b = np.ascontiguousarray(blocks, dtype=np.uint8)
         self._chk(self.lib.ms_load_weight_q(self.h, tensor, layer, ggml_type, b.ctypes.data, b.size),
                   "ms_load_weight_q")
+
+    def weight_regions(self) -> list:
+        """[(device pointer, bytes)] of every weight buffer, in the engine's fixed order."""
+        n = self._chk(self.lib.ms_weight_regions(self.h, None, None, 0), "ms_weight_regions")
+        ptrs, sizes = (C.c_void_p * n)(), (C.c_int64 * n)()
+        self._chk(self.lib.ms_weight_regions(self.h, ptrs, sizes, n), "ms_weight_regions")
+        return [(int(ptrs[i] or 0), int(sizes[i])) for i in range(n)]
+
+    def quant_manifest(self) -> list:
+        n = self._chk(self.lib.ms_quant_manifest(self.h, None, 0), "ms_quant_manifest")
+        buf = (C.c_int32 * (3 * max(n, 1)))()
+        self._chk(self.lib.ms_quant_manifest(self.h, buf, n), "ms_quant_manifest")
+        return [tuple(buf[3 * i:3 * i + 3]) for i in range(n)]
+
+    def declare_weight_q(self, tensor: int, layer: int, ggml_type: int):
+        self._chk(self.lib.ms_declare_weight_q(self.h, tensor, layer, ggml_type), "ms_declare_weight_q")
 
     def load_tensor(self, tensor: int, layer: int, bf16_bits: np.ndarray):
         a = np.ascontiguousarray(bf16_bits, dtype=np.uint16)

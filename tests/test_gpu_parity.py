@@ -656,3 +656,34 @@ def test_quantized_engine_greedy_vs_oracle(dev):
         assert rel(lg, ref_lg) < 2e-2
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("quant", [False, True])
+def test_weight_regions_are_the_whole_model(dev, quant):
+    """What a weight broadcast moves (mapsum.dist.broadcast_engine_weights): an engine that
+    only declared the K-quant layout and received every region of another engine's weights
+    (a device copy standing in for the RCCL broadcast) generates the same tokens."""
+    from mapsum.dist import region_views
+    a = Engine(TINY, device=0, max_batch=4, max_ctx=256, max_prefill_tokens=1024)
+    b = Engine(TINY, device=0, max_batch=4, max_ctx=256, max_prefill_tokens=1024)
+    try:
+        if quant:
+            a.init_synthetic_q(seed=9, scale=0.05, norm_jitter=0.1)
+        else:
+            a.init_synthetic(SEED, STD, JITTER)
+        for t, l, ty in a.quant_manifest():
+            b.declare_weight_q(t, l, ty)
+        va, vb = region_views(a), region_views(b)
+        assert [v.numel() for v in va] == [v.numel() for v in vb]
+        for x, y in zip(va, vb):
+            y.copy_(x)
+        torch.cuda.synchronize()
+        prompts = [_prompt(n, 60 + n) for n in (5, 77, 130)]
+        ra = a.generate(prompts, num_predict=12, ignore_eos=True)
+        rb = b.generate(prompts, num_predict=12, ignore_eos=True)
+        assert [r.ids for r in ra] == [r.ids for r in rb]
+        if quant:
+            assert len(a.quant_manifest()) == 7 * TINY.n_layers + 1
+    finally:
+        a.close()
+        b.close()

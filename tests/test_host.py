@@ -303,3 +303,55 @@ def test_cabi_errors_without_gpu():
     assert b"abi_version" in lib.ms_last_error(None)
     assert lib.ms_step(None) == _lib.MS_EINVAL
     assert lib.ms_op_gemv_workspace(0, 16, 64) == _lib.MS_EINVAL
+
+
+class _HostWeights:
+    """CPU stand-in for an engine's weight regions and K-quant manifest."""
+
+    def __init__(self, rank):
+        import torch
+        self.regions = [torch.full((n,), rank + 1, dtype=torch.uint8) for n in (7, 1024, 3)]
+        self.manifest = [(2, 0, 12), (9, 1, 14)] if rank == 0 else []
+        self.declared = []
+
+    def quant_manifest(self):
+        return list(self.manifest)
+
+    def declare_weight_q(self, t, l, ty):
+        self.declared.append((t, l, ty))
+        self.regions.append(__import__("torch").zeros(16, dtype=__import__("torch").uint8))
+
+    def region_views(self):
+        return self.regions
+
+
+def _bcast_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from mapsum.dist import broadcast_engine_weights
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    e = _HostWeights(rank)
+    if rank == 0:  # rank 0's quantised regions exist already
+        e.regions += [__import__("torch").full((16,), 9, dtype=__import__("torch").uint8) for _ in range(2)]
+    n = broadcast_engine_weights(e, src=0)
+    q.put((rank, n, e.declared, [r.tolist() for r in e.regions]))
+    dist.destroy_process_group()
+
+
+def test_weight_broadcast_gloo_world2():
+    """Rank 0's weights (and its K-quant layout) reach the other rank byte for byte."""
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict((r, (n, d, regs)) for r, n, d, regs in (q.get(timeout=120) for _ in range(2)))
+    for p in ps:
+        p.join(60)
+    assert got[1][1] == [(2, 0, 12), (9, 1, 14)]  # the receiver declared rank 0's layout
+    assert got[0][2] == got[1][2] and got[0][0] == got[1][0] == 7 + 1024 + 3 + 32
