@@ -11,13 +11,20 @@
 //   * a bf16 copy = bf16_rne(dequant(blocks)) in the fused row layout, for prefill GEMMs
 //     and the embedding gather (compute-bound; bf16 is what MFMA consumes), and
 //   * the quantised rows for decode, which is HBM-bound: 4.5 / 6.56 bits per weight
-//     instead of 16.  Q4_K rows keep the ggml block layout (144 B = 9 x 16 B, aligned);
-//     Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales 16 | d 2 + pad] so every
-//     field is 16-B aligned.
+//     instead of 16.  Q4_K blocks keep their 16-B ggml header (d, dmin, 12 scale bytes) and
+//     144 B, but the 128 quant bytes are re-ordered so that lane group g of a wave reads,
+//     as 32 contiguous bytes, one dword per sub-block s holding weights 32s+8g .. +7 (byte i =
+//     q[k_i] | q[k_{i+4}] << 4); Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales
+//     16 | d 2 + pad] so every field is 16-B aligned.
 // The fused GEMV streams the blocks HBM -> VGPR (one super-block of 256 weights per row
-// per wave-step), dequantises in registers to exactly the bf16 values of the bf16 copy,
-// and feeds v_mfma_f32_16x16x32_bf16 -- decode with Q4_K_M weights therefore computes
-// the same model as prefill, only from 3.6x fewer weight bytes.
+// per wave-step) and feeds v_mfma_f32_16x16x32_bf16:
+//   * Q4_K, one MFMA per 32-weight sub-block: the nibbles become bf16 (128 + q) by a byte
+//     permute against 0x43 (exact integers), the MFMA gives A_s = sum_k x_k (128 + q_k), and
+//     sum_k x_k y_k = d_s A_s - (128 d_s + m_s) X_s with d_s = d*sc_s, m_s = dmin*m_s (ggml's
+//     fp32 d1 / m1) and X_s = sum of the sub-block's x (from LDS) -- 2 FMAs per output
+//     element per sub-block instead of dequantising every weight: the decode GEMV uses the
+//     exact fp32 dequantised weights (no bf16 rounding of them);
+//   * Q6_K, dequantised in registers to the bf16 values of the bf16 copy.
 #include <cstdlib>
 
 #include "gemv_common.h"
@@ -99,8 +106,22 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
   if (dst_q) {
     const int bp = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KPacked;
     uint8_t* q = dst_q + ((drow - q_row_base) * nsb + sb) * bp;
-    if (t < braw) q[t] = b[t];  // Q6_K: same field order, d at 208, tail padded below
-    if (type == MS_QT_Q6_K && t >= braw && t < kQ6KPacked) q[t] = 0;
+    if (type == MS_QT_Q4_K) {
+      // header as is; quant byte 16 + 4(8g + s) + i = q[k] | q[k + 4] << 4, k = 32s + 8g + i
+      if (t < 16) q[t] = b[t];
+      if (t < 128) {
+        const int g = t >> 5, s_ = (t >> 2) & 7, i = t & 3;
+        auto nib = [&](int k) {
+          const uint32_t qb = b[16 + (k >> 6) * 32 + (k & 31)];
+          return ((k & 63) >> 5) ? (qb >> 4) : (qb & 0xF);
+        };
+        const int k = 32 * s_ + 8 * g + i;
+        q[16 + t] = (uint8_t)(nib(k) | (nib(k + 4) << 4));
+      }
+    } else {
+      if (t < braw) q[t] = b[t];  // Q6_K: same field order, d at 208, tail padded below
+      if (t >= braw && t < kQ6KPacked) q[t] = 0;
+    }
   }
 }
 
@@ -205,39 +226,63 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
       gemv_stage_x(smem, X, M, K, ldx);
       __syncthreads();
     }
+    // X_s: the sum of each row's x over each 32-weight sub-block of this block's K range,
+    // [sub-block][16*MT rows] fp32 after the X image (rows >= M: 0), fixed summation order
+    const int nsub = K / 32;
+    float* xsum = (float*)(smem + (XL ? (size_t)M * xstride : 0));
+    for (int e = threadIdx.x; e < nsub * 16 * MT; e += blockDim.x) {
+      const int sidx = e / (16 * MT), r = e - sidx * (16 * MT);
+      float a = 0.f;
+      if (r < M) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bf16x8 v = XL ? *(const bf16x8*)(smem + r * xstride + (sidx * 32 + 8 * c) * 2)
+                              : *(const bf16x8*)(X + (size_t)r * ldx + sidx * 32 + 8 * c);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) a += (float)v[i];
+        }
+      }
+      xsum[sidx * 16 * MT + r] = a;
+    }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const float d = h2f(hq[j][n].x), dmin = h2f(hq[j][n].x >> 16);
-        int s0, m0, s1, m1;
-        scale_min_k4(hq[j][n], 2 * g, s0, m0);
-        scale_min_k4(hq[j][n], 2 * g + 1, s1, m1);
-        const float dl[2] = {__fmul_rn(d, (float)s0), __fmul_rn(d, (float)s1)};
-        const float ml[2] = {__fmul_rn(dmin, (float)m0), __fmul_rn(dmin, (float)m1)};
+        const uint4 h = hq[j][n];
+        const float d = h2f(h.x), dmin = h2f(h.x >> 16);
+        // get_scale_min_k4 for all 8 sub-blocks at once, one byte each
+        const uint32_t sc03 = h.y & 0x3F3F3F3Fu, m03 = h.z & 0x3F3F3F3Fu;
+        const uint32_t sc47 = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+        const uint32_t m47 = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+        const uint32_t qw[8] = {q0[j][n].x, q0[j][n].y, q0[j][n].z, q0[j][n].w,
+                                q1[j][n].x, q1[j][n].y, q1[j][n].z, q1[j][n].w};
 #pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const int h = t >> 2, c = t & 3;
-          const uint4& qq = (c < 2) ? q0[j][n] : q1[j][n];
-          const uint32_t w0 = (c & 1) ? qq.z : qq.x, w1 = (c & 1) ? qq.w : qq.y;
-          uint32_t pk[4];
-#pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            const uint32_t wd = (i < 4) ? w0 : w1;
-            const uint32_t b0 = (wd >> (8 * (i & 3))) & 0xFF, b1 = (wd >> (8 * ((i + 1) & 3))) & 0xFF;
-            const uint32_t n0q = h ? (b0 >> 4) : (b0 & 0xF), n1q = h ? (b1 >> 4) : (b1 & 0xF);
-            const float y0 = __fsub_rn(__fmul_rn(dl[h], (float)n0q), ml[h]);
-            const float y1 = __fsub_rn(__fmul_rn(dl[h], (float)n1q), ml[h]);
-            pk[i >> 1] = pack2bf(y0, y1);
-          }
+        for (int s_ = 0; s_ < 8; ++s_) {
+          const uint32_t scw = s_ < 4 ? sc03 : sc47, mw = s_ < 4 ? m03 : m47;
+          const int sh = 8 * (s_ & 3);
+          const float d1 = __fmul_rn(d, (float)((scw >> sh) & 0xFFu));   // ggml d1 = d * sc
+          const float m1 = __fmul_rn(dmin, (float)((mw >> sh) & 0xFFu));  // ggml m1 = dmin * m
+          const float c1 = __fmaf_rn(128.0f, d1, m1);                      // 128 d1 + m1 (exact 128 d1)
+          const uint32_t lo = qw[s_] & 0x0F0F0F0Fu, hi = (qw[s_] >> 4) & 0x0F0F0F0Fu;
+          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+          // bytes [q, 0x43, q', 0x43] = bf16 (128 + q, 128 + q'): weights k .. k+7 in order
+          const u4v pk = {__builtin_amdgcn_perm(0x43434343u, lo, 0x04010400u),
+                          __builtin_amdgcn_perm(0x43434343u, lo, 0x04030402u),
+                          __builtin_amdgcn_perm(0x43434343u, hi, 0x04010400u),
+                          __builtin_amdgcn_perm(0x43434343u, hi, 0x04030402u)};
           const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
-          const int k = (sb0 + j) * 256 + g * 64 + h * 32 + c * 8;
+          const int ks = (sb0 + j) * 8 + s_;  // sub-block index in this block's K range
+          const int k = ks * 32 + 8 * g;
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
             const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
                                  : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
-            acc[m][n] = mfma16(xf, wf, acc[m][n]);
+            const f32x4 A = mfma16(xf, wf, f32x4{0.f, 0.f, 0.f, 0.f});
+            const f32x4 xs = *(const f32x4*)(xsum + ks * 16 * MT + m * 16 + 4 * g);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[m][n][i] = __fmaf_rn(-c1, xs[i], __fmaf_rn(d1, A[i], acc[m][n][i]));
           }
         }
       }
@@ -311,7 +356,7 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
   const int nsb = K / 256;
   p.SBW = nsb > 16 ? 2 : 1;
   static const int env_sbw = [] { const char* v = getenv("MS_QSBW"); return v ? atoi(v) : 0; }();
-  if ((env_sbw == 1 || env_sbw == 2) && nsb % env_sbw == 0 && nsb / env_sbw <= 16) p.SBW = env_sbw;  // tuning hook
+  if (env_sbw >= 1 && env_sbw <= 4 && nsb % env_sbw == 0 && nsb / env_sbw <= 16) p.SBW = env_sbw;  // tuning hook
   p.waves = (nsb % p.SBW == 0) ? nsb / p.SBW : 0;
   if (p.waves > 16) p.waves = 0;
   return p;
@@ -319,10 +364,13 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
 
 static constexpr size_t kLdsCap = 160 * 1024;
 
-static bool qx_in_lds(int M, int K) { return (size_t)M * (2 * (size_t)K + 16) <= kLdsCap; }
+static bool qx_in_lds(int M, int K) {
+  return (size_t)M * (2 * (size_t)K + 16) + (size_t)(K / 32) * 16 * ((M + 15) / 16) * 4 <= kLdsCap;
+}
 
 static size_t qlds(const QPlan& p, int M, int K) {
-  const size_t xs = qx_in_lds(M, K) ? (size_t)M * (2 * (size_t)K + 16) : 0;
+  // X image (when it fits) + the Q4_K sub-block sums [K/32][16*MT] fp32
+  const size_t xs = (qx_in_lds(M, K) ? (size_t)M * (2 * (size_t)K + 16) : 0) + (size_t)(K / 32) * 16 * p.MT * 4;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
@@ -345,7 +393,11 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
     const bool xl = qx_in_lds(M, K);
 #define QL(SBW_, XL_) \
     MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XL_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
-    if (p.SBW == 2 && xl) QL(2, true);
+    if (p.SBW == 4 && xl) QL(4, true);
+    else if (p.SBW == 4) QL(4, false);
+    else if (p.SBW == 3 && xl) QL(3, true);
+    else if (p.SBW == 3) QL(3, false);
+    else if (p.SBW == 2 && xl) QL(2, true);
     else if (p.SBW == 2) QL(2, false);
     else if (xl) QL(1, true);
     else QL(1, false);

@@ -273,6 +273,7 @@ def test_qgemv_bench_shapes(dev, qtype, N, K, epi):
     from oracle import quants as Q
     lib = L.load()
     M = 8
+    qt = qtype
     b = Q.random_blocks(qtype, N * K // 256, seed=N + K, scale=0.02)
     bd = torch.from_numpy(b.reshape(-1)).to(dev)
     wbf = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
@@ -280,7 +281,9 @@ def test_qgemv_bench_shapes(dev, qtype, N, K, epi):
     L.check(lib.ms_op_quant_rows(qtype, bd.data_ptr(), N, K, wbf.data_ptr(), pk.data_ptr(), _stream()))
     g = torch.Generator(device="cuda").manual_seed(K)
     X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
-    ref = X.double() @ wbf.double().T
+    # Q4_K: the decode GEMV computes with the exact fp32 dequant; Q6_K: with the bf16 copy
+    wd = torch.from_numpy(Q.c_dequant(b, qt).reshape(N, K)).to(dev).double() if qt == 12 else wbf.double()
+    ref = X.double() @ wd.T
     if epi == L.MS_EPI_SWIGLU:
         out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
         r = ref.view(M, N // 32, 2, 16)

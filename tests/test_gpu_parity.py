@@ -512,6 +512,15 @@ def test_dequant_bit_exact_vs_c_oracle(lib, dev, qtype):
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), "dequant must be bit-exact"
 
 
+def _decode_weights(qtype, b, wbf):
+    """The weights the decode GEMV computes with: Q4_K -- the exact fp32 dequantisation
+    (the kernel applies d1 / m1 per sub-block after an MFMA on the integer quants); Q6_K --
+    the bf16 copy (dequantised to bf16 in registers)."""
+    if qtype == Q.GGML_TYPE_Q4_K:
+        return torch.from_numpy(Q.c_dequant(b, qtype).reshape(wbf.shape)).double()
+    return wbf.double().cpu()
+
+
 def _packed(lib, dev, qtype, rows, K, seed):
     b = Q.random_blocks(qtype, rows * K // 256, seed=seed)
     bd = torch.from_numpy(b.reshape(-1)).to(dev)
@@ -536,12 +545,12 @@ def test_quant_rows_bf16_copy_is_rounded_dequant(lib, dev, qtype):
 @pytest.mark.parametrize("N,K,epi", [(256, 768, L.MS_EPI_STORE_BF16), (512, 2048, L.MS_EPI_ADD_F32),
                                      (1024, 768, L.MS_EPI_SWIGLU), (128, 8192, L.MS_EPI_STORE_F32)])
 def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
-    _, wbf, pk = _packed(lib, dev, qtype, N, K, 7 + M)
+    b, wbf, pk = _packed(lib, dev, qtype, N, K, 7 + M)
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
     # fp64 reference on the host: fp32 outputs may differ only by summation order, bf16
     # outputs additionally by one rounding
-    ref = (X.double().cpu() @ wbf.double().cpu().T).to(dev)
+    ref = (X.double().cpu() @ _decode_weights(qtype, b, wbf).T).to(dev)
     tol = 2e-6 if epi in (L.MS_EPI_STORE_F32, L.MS_EPI_ADD_F32) else 4e-3
     if epi == L.MS_EPI_SWIGLU:
         out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
@@ -569,14 +578,14 @@ def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
 def test_qgemv_split_slabs_vs_fp64(lib, dev, qtype, M, N, K, S):
     """Quantised split-K: slab s is the dequantised partial product over its K range (fp32
     sum order only); the slabs add up to the full product; bad splits are refused."""
-    _, wbf, pk = _packed(lib, dev, qtype, N, K, 11 + M + S)
+    b, wbf, pk = _packed(lib, dev, qtype, N, K, 11 + M + S)
     g = torch.Generator(device="cpu").manual_seed(M + N + K + S)
     X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
     slabs = torch.full((S, M, N), float("nan"), device=dev)
     L.check(lib.ms_op_qgemv_split(X.data_ptr(), qtype, pk.data_ptr(), slabs.data_ptr(), M, N, K, S,
                                   _stream()))
     torch.cuda.synchronize()
-    Xd, Wd, ks = X.double().cpu(), wbf.double().cpu(), K // S
+    Xd, Wd, ks = X.double().cpu(), _decode_weights(qtype, b, wbf), K // S
     for s_ in range(S):
         exp = Xd[:, s_ * ks:(s_ + 1) * ks] @ Wd[:, s_ * ks:(s_ + 1) * ks].T
         assert rel(slabs[s_].double().cpu(), exp) < 2e-6, s_

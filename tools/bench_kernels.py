@@ -12,6 +12,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "map-reduced-approach-for-vietnamese-long-document-summarization_amd"))
+sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -142,6 +143,52 @@ def bench_dgemm(lib):
             print(line, flush=True)
 
 
+def bench_qgemv(lib, M):
+    """Dequant-fused decode GEMV (k_qgemv.hip) on the Q4_K_M shapes at M rows: plain launch
+    and split-K slabs over S, on > 512 MB rotations of packed weights (no MALL reuse).
+    GB/s = compressed weight bytes / time."""
+    from oracle import quants as Q
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, N, K, qt, epi in [("qkv", 5120, 3072, 12, 3), ("o", 3072, 3072, 12, 1), ("gu", 16384, 3072, 12, 2),
+                                ("down", 3072, 8192, 12, 1), ("down6", 3072, 8192, 14, 1),
+                                ("lm_head6", 128256, 3072, 14, 3)]:
+        bpb = 144 if qt == 12 else 224
+        nbytes = N * (K // 256) * bpb
+        b = Q.random_blocks(qt, min(N, 4096) * K // 256, seed=1, scale=0.02)
+        bd = torch.from_numpy(b.reshape(-1)).to(dev)
+        rows_src = min(N, 4096)
+        pks = []
+        for _ in range(max(2, -(-512 * 2**20 // nbytes))):
+            pk = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            wbf = torch.empty(rows_src, K, dtype=torch.bfloat16, device=dev)
+            for r0 in range(0, N, rows_src):  # tile the random rows over the matrix
+                rr = min(rows_src, N - r0)
+                tmp = torch.empty(rr * (K // 256) * bpb, dtype=torch.uint8, device=dev)
+                lib.ms_op_quant_rows(qt, bd.data_ptr(), rr, K, wbf.data_ptr(), tmp.data_ptr(), st)
+                pk[r0 * (K // 256) * bpb:(r0 + rr) * (K // 256) * bpb] = tmp
+            pks.append(pk)
+        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        out = torch.zeros(8 * M * N, device=dev)
+        ldo = N // 2 if epi == 2 else N
+        i = [0]
+
+        def nextp():
+            i[0] += 1
+            return pks[i[0] % len(pks)]
+        line = f"{name:8s} N={N:6d} K={K:5d} M={M:2d} {nbytes/1e6:6.1f} MB |"
+        t = timeit(lambda: lib.ms_op_qgemv(X.data_ptr(), qt, nextp().data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st))
+        line += f" plain {t*1e3:6.1f}us {nbytes/t/1e6:5.0f} |"
+        if epi != 2:
+            for S in (2, 3, 4, 6, 8):
+                if (K // 256) % S:
+                    continue
+                t = timeit(lambda: lib.ms_op_qgemv_split(X.data_ptr(), qt, nextp().data_ptr(), out.data_ptr(), M, N, K,
+                                                         S, st))
+                line += f" S{S} {t*1e3:6.1f}us {nbytes/t/1e6:5.0f} |"
+        print(line, flush=True)
+
+
 def bench_gemm(lib):
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -166,7 +213,7 @@ def bench_gemm(lib):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv"])
     ap.add_argument("--m", type=int, default=8)
     a = ap.parse_args()
     lib = L.load()
@@ -178,5 +225,7 @@ if __name__ == "__main__":
         bench_split(lib, a.m)
     elif a.what == "dgemm":
         bench_dgemm(lib)
+    elif a.what == "qgemv":
+        bench_qgemv(lib, a.m)
     else:
         bench_gemm(lib)
