@@ -6,6 +6,18 @@ namespace ms {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *(const uint4*)p; }
 
+// once-read decode streams (weights, KV pages): non-temporal loads when MS_NT_STREAM is set
+// (MI355X_MICROARCH.md 'nt-weights': a decode weight stream read once per step)
+__device__ __forceinline__ uint4 ldw16(const void* p) {
+#ifdef MS_NT_STREAM
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load((const v4u*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *(const uint4*)p;
+#endif
+}
+
 // X rows [M][K] bf16 (row stride ldx elements) -> LDS, row stride 2K+16 bytes (the 16-B
 // skew puts the 16 rows of an MFMA fragment read on different banks).  Caller synchronises.
 __device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restrict__ X, int M, int K,

@@ -47,6 +47,15 @@ __device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
 
 // one 64-key K/V tile (16 KB each) into registers, 4 x 16 B per thread, coalesced rows
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// decode KV pages are read once per step: non-temporal when MS_NT_STREAM is set
+__device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
+#ifdef MS_NT_STREAM
+  return __builtin_nontemporal_load((const u32x4*)p);
+#else
+  return *(const u32x4*)p;
+#endif
+}
+
 __device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], const KVView& kv,
                                               const int32_t* bt, int kvh, int t, int kvlen,
                                               int tid) {
@@ -68,36 +77,53 @@ __device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], co
 }
 
 // ============================================================ prefill (varlen, causal)
-// grid (n_qblk, Hq); block 256 = 4 waves x 16 query rows of one head; KV tiles of 64.
-__global__ __launch_bounds__(256) void attn_prefill_kernel(const bf16_t* __restrict__ qkv,
-                                                           bf16_t* __restrict__ out, int Hq,
-                                                           int Hk, KVView kv, PrefillAttnArgs a,
-                                                           float scale_log2) {
+// 1-D grid over (q-block, head group), heaviest q-blocks first for every head group; block
+// 256 = 4 waves x 16 query rows, GB q heads of ONE kv head (GQA group, or a divisor of it).
+// Each K fragment read from LDS feeds GB MFMAs (S^T of the GB heads) and each V^T fragment
+// GB MFMAs (O^T of the GB heads): LDS read traffic per MFMA drops GB-fold, and a K/V tile
+// is fetched from HBM once per GB heads instead of once per head.  The online softmax works
+// on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)); the O rescale is skipped when no
+// query column of the wave raised its max (alpha == 1 exactly); the causal / sequence-end
+// mask is applied only on tiles that can cross it.
+template <int GB>
+__global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __restrict__ qkv,
+                                                              bf16_t* __restrict__ out, int Hq,
+                                                              int Hk, KVView kv, PrefillAttnArgs a,
+                                                              float scale_log2) {
   __shared__ __attribute__((aligned(16))) char smem[32768];
   char* ks_ = smem;
   char* vs_ = smem + 16384;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
-  const int h = blockIdx.y;
-  const int e = a.qblk[blockIdx.x];
+  const int ngrp = Hq / GB;
+  const int e = a.qblk[blockIdx.x / ngrp];
+  const int h0 = (blockIdx.x % ngrp) * GB;
   const int sq = e >> 16, qb = e & 0xFFFF;
   const int qlen = a.seq_qlen[sq], kvlen = a.seq_kvlen[sq], qstart = a.seq_qstart[sq];
   const int slot = a.seq_slot[sq];
-  const int kvh = h / (Hq / Hk);
+  const int kvh = h0 / (Hq / Hk);
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
   const int qi = qb * 64 + wave * 16 + r;
   const int qpos = kvlen - qlen + qi;
+  const int wave_qpos0 = kvlen - qlen + qb * 64 + wave * 16;  // the wave's first query
 
-  bf16x8 qf[4];
+  bf16x8 qf[GB][4];
   {
-    const bf16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h * kHeadDim;
+    const bf16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h0 * kHeadDim;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) qf[s] = as_bf16x8(*(const uint4*)(qrow + 32 * s + 8 * g));
+    for (int hh = 0; hh < GB; ++hh)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) qf[hh][s] = as_bf16x8(*(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g));
   }
-  f32x4 o[8];
+  f32x4 o[GB][8];
+  float m_run[GB], l_run[GB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  for (int hh = 0; hh < GB; ++hh) {
+    m_run[hh] = -INFINITY;
+    l_run[hh] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[hh][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int q_last = min(qb * 64 + 63, qlen - 1);
   const int kv_end = kvlen - qlen + q_last + 1;  // keys visible to the block's last query
@@ -122,62 +148,91 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(const bf16_t* __restr
     __syncthreads();
     if (t + 1 < ntiles) fetch_kv_tile(kreg, vreg, kv, bt, kvh, t + 1, kvlen, tid);  // next tile's HBM reads overlap this tile's math
 
-    f32x4 sc[4];
+    f32x4 sc[GB][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
-      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int hh = 0; hh < GB; ++hh) sc[hh][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int krow = mt * 16 + r;
-        const bf16x8 kf = *(const bf16x8*)(ks_ + k_swz(krow, 4 * s + g));
-        sc[mt] = mfma16(kf, qf[s], sc[mt]);
+        const bf16x8 kf = *(const bf16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
+#pragma unroll
+        for (int hh = 0; hh < GB; ++hh) sc[hh][mt] = mfma16(kf, qf[hh][s], sc[hh][mt]);
       }
     }
-    float mx = -INFINITY;
+    // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
+    // first query or the sequence end can hold any
+    const bool masked = (t * 64 + 63 > wave_qpos0) || (t * 64 + 64 > kvlen);
+    if (masked) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = t * 64 + mt * 16 + 4 * g + j;
-        const float v = (key > qpos || key >= kvlen) ? -INFINITY : sc[mt][j] * scale_log2;
-        sc[mt][j] = v;
-        mx = fmaxf(mx, v);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
-    float rs = 0.f;
+        for (int j = 0; j < 4; ++j) {
+          const int key = t * 64 + mt * 16 + 4 * g + j;
+          if (key > qpos || key >= kvlen)
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - m_new);
-        sc[mt][j] = p;
-        rs += p;
-      }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
-#pragma unroll
-    for (int kstep = 0; kstep < 2; ++kstep) {
-      const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
-#pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
+            for (int hh = 0; hh < GB; ++hh) sc[hh][mt][j] = -INFINITY;
+        }
     }
+    bf16x8 pf[GB][2];
+    bool rescale = false;
+    float alpha[GB];
+#pragma unroll
+    for (int hh = 0; hh < GB; ++hh) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sc[hh][mt][j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[hh], mx);
+      alpha[hh] = (m_run[hh] == m_new) ? 1.f : __builtin_amdgcn_exp2f((m_run[hh] - m_new) * scale_log2);
+      rescale |= (m_run[hh] != m_new);
+      const float mc = (m_new == -INFINITY) ? 0.f : m_new * scale_log2;
+      float rs = 0.f;
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = __builtin_amdgcn_exp2f(__fmaf_rn(sc[hh][mt][j], scale_log2, -mc));
+          sc[hh][mt][j] = p;
+          rs += p;
+        }
+      rs += __shfl_xor(rs, 16, 64);
+      rs += __shfl_xor(rs, 32, 64);
+      l_run[hh] = l_run[hh] * alpha[hh] + rs;
+      m_run[hh] = m_new;
+      pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
+      pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
+    }
+    if (__ballot(rescale) != 0) {
+#pragma unroll
+      for (int hh = 0; hh < GB; ++hh)
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[hh][dt] *= alpha[hh];
+    }
+#pragma unroll
+    for (int kstep = 0; kstep < 2; ++kstep)
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const bf16x8 vt = load_vt(vs_, dt, kstep, lane);
+#pragma unroll
+        for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
+      }
   }
   if (qi < qlen) {
-    const float inv = 1.0f / l_run;
-    bf16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + h * kHeadDim;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      uint2 w;
-      w.x = pack2bf(o[dt][0] * inv, o[dt][1] * inv);
-      w.y = pack2bf(o[dt][2] * inv, o[dt][3] * inv);
-      *(uint2*)(orow + dt * 16 + 4 * g) = w;
+    for (int hh = 0; hh < GB; ++hh) {
+      const float inv = 1.0f / l_run[hh];
+      bf16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + (h0 + hh) * kHeadDim;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        uint2 w;
+        w.x = pack2bf(o[hh][dt][0] * inv, o[hh][dt][1] * inv);
+        w.y = pack2bf(o[hh][dt][2] * inv, o[hh][dt][3] * inv);
+        *(uint2*)(orow + dt * 16 + 4 * g) = w;
+      }
     }
   }
 }
@@ -186,8 +241,14 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
                          PrefillAttnArgs a, hipStream_t s) {
   if (a.n_qblk <= 0) return;
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
-  MS_LAUNCH(attn_prefill_kernel, dim3(a.n_qblk, Hq), dim3(256), 0, s, qkv, out, Hq, Hk,
-                     kv, a, scale_log2);
+  const int G = Hq / Hk;
+  const int gb = (G % 3 == 0) ? 3 : (G % 2 == 0) ? 2 : 1;
+  const dim3 grid(a.n_qblk * (Hq / gb));
+#define AP(GB_) MS_LAUNCH(attn_prefill_kernel<GB_>, grid, dim3(256), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
+  if (gb == 3) AP(3);
+  else if (gb == 2) AP(2);
+  else AP(1);
+#undef AP
 }
 
 // ============================================================ decode (split-K over keys)
@@ -268,13 +329,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
-        kf[mt][s4] = *(const u32x4*)(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
+        kf[mt][s4] = ld_stream(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
   };
   auto fetch_v = [&](int pg) {
     const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
-      vr[i] = *(const u32x4*)(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
+      vr[i] = ld_stream(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
   };
   // issue the first page first, so its HBM latency overlaps the q/k/v prologue
   if (pg0 * kPage < len) {

@@ -60,8 +60,8 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(const bf16_t* __restrict_
 #pragma unroll
   for (int p = 0; p < DPF - 1; ++p)
     if (p < nk) {
-      wr[p][0] = ldg16(wrow + p * DBK);
-      wr[p][1] = ldg16(wrow + p * DBK + 8);
+      wr[p][0] = ldw16(wrow + p * DBK);
+      wr[p][1] = ldw16(wrow + p * DBK + 8);
     }
   stage_x(0, 0);
 
@@ -76,8 +76,8 @@ __global__ __launch_bounds__(256, 2) void dgemm_kernel(const bf16_t* __restrict_
     // ops issued after it are pending
     const bool wmore = t + DPF - 1 < nk, more = t + 1 < nk;
     if (wmore) {
-      wr[(t + DPF - 1) % DPF][0] = ldg16(wrow + (t + DPF - 1) * DBK);
-      wr[(t + DPF - 1) % DPF][1] = ldg16(wrow + (t + DPF - 1) * DBK + 8);
+      wr[(t + DPF - 1) % DPF][0] = ldw16(wrow + (t + DPF - 1) * DBK);
+      wr[(t + DPF - 1) % DPF][1] = ldw16(wrow + (t + DPF - 1) * DBK + 8);
     }
     if (more) stage_x(buf ^ 1, (t + 1) * DBK);
     if (wmore) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 + XI));

@@ -89,8 +89,8 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     const bf16_t* wp = W + (size_t)min(n0 + n * 16 + fr, N - 1) * ldk + kbeg + 16 * fg;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      w[u][n][0] = ldg16(wp + u * 64);
-      w[u][n][1] = ldg16(wp + u * 64 + 8);
+      w[u][n][0] = ldw16(wp + u * 64);
+      w[u][n][1] = ldw16(wp + u * 64 + 8);
     }
   }
   // 2. stage the M rows of X into LDS (XL) -- or read fragments from L2 (large M*K)

@@ -218,9 +218,9 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ4KBytes;
-        hq[j][n] = ldg16(bp);
-        q0[j][n] = ldg16(bp + 16 + 32 * g);
-        q1[j][n] = ldg16(bp + 32 + 32 * g);
+        hq[j][n] = ldw16(bp);
+        q0[j][n] = ldw16(bp + 16 + 32 * g);
+        q1[j][n] = ldw16(bp + 32 + 32 * g);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
       gemv_stage_x(smem, X, M, K, ldx);
@@ -295,10 +295,10 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ6KPacked;
-        qa[j][n] = ldg16(bp + hh * 64 + 16 * p);
-        qb[j][n] = ldg16(bp + hh * 64 + 32 + 16 * p);
-        qh[j][n] = ldg16(bp + 128 + hh * 32 + 16 * p);
-        sc[j][n] = ldg16(bp + 192);
+        qa[j][n] = ldw16(bp + hh * 64 + 16 * p);
+        qb[j][n] = ldw16(bp + hh * 64 + 32 + 16 * p);
+        qh[j][n] = ldw16(bp + 128 + hh * 32 + 16 * p);
+        sc[j][n] = ldw16(bp + 192);
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
     if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmapsum.so")
+# MAPSUM_LIB: an alternative in-tree build of the same library (A/B timing of build variants)
+LIB_PATH = os.environ.get("MAPSUM_LIB") or os.path.join(_HERE, "libmapsum.so")
 
 MS_ABI_VERSION = 2
 MS_OK, MS_EIO, MS_ENOMEM, MS_EBUSY, MS_EINVAL, MS_ENOSPC = 0, -5, -12, -16, -22, -28
