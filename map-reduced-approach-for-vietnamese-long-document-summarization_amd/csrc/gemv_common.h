@@ -18,15 +18,30 @@ __device__ __forceinline__ uint4 ldw16(const void* p) {
 #endif
 }
 
-// X rows [M][K] bf16 (row stride ldx elements) -> LDS, row stride 2K+16 bytes (the 16-B
-// skew puts the 16 rows of an MFMA fragment read on different banks).  Caller synchronises.
-__device__ __forceinline__ void gemv_stage_x(char* smem, const bf16_t* __restrict__ X, int M, int K,
-                                             int ldx) {
-  const size_t xstride = 2 * (size_t)K + 16;
-  const int kch = K / 8;  // 16-B chunks per row
-  for (int c = threadIdx.x; c < M * kch; c += blockDim.x) {
-    const int r = c / kch, k8 = c - r * kch;
-    *(uint4*)(smem + r * xstride + k8 * 16) = ldg16(X + (size_t)r * ldx + k8 * 8);
+// s_waitcnt immediate for vmcnt(n) with expcnt/lgkmcnt left alone (gfx9 encoding)
+__host__ __device__ constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// X rows [M][K] bf16 (row stride ldx elements) -> LDS image of M rows x 2K bytes, 16-B
+// chunk c of row r stored at chunk c ^ (r & 7) (the rows of an MFMA fragment read land on
+// different bank groups).  Copied by LDS DMA (global_load_lds, 1 KiB per wave instruction)
+// and issued BEFORE the weight stream: vmcnt retires loads in issue order, so X loaded
+// after the weights would hold the image -- and every wave of the block, at the barrier --
+// until the block's whole weight stream had landed, serialising all the dequant / MFMA work
+// behind the memory phase; the DMA needs no registers (a register copy cost the GEMVs
+// occupancy).  The caller waits vmcnt(<its weight loads>) and synchronises.  K % 64 == 0;
+// the image is padded to whole KiB (the last piece's spare lanes land there).
+__host__ __device__ inline size_t gemv_x_lds_bytes(int M, int K) {
+  return ((size_t)M * K * 2 + 1023) / 1024 * 1024;
+}
+__device__ __forceinline__ int x_lds(int r, int k, int K) { return r * 2 * K + (((k >> 3) ^ (r & 7)) << 4); }
+
+__device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict__ X, int M, int K, int ldx) {
+  const int kch = K >> 3, n = M * kch, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  for (int p = threadIdx.x >> 6; p * 64 < n; p += nw) {
+    const int P = min(p * 64 + lane, n - 1);
+    const int r = P / kch, c = P - r * kch;
+    __builtin_amdgcn_global_load_lds((const void*)(X + (size_t)r * ldx + ((c ^ (r & 7)) << 3)),
+                                     (LDS_AS void*)(smem + (size_t)p * 1024), 16, 0, 0);
   }
 }
 

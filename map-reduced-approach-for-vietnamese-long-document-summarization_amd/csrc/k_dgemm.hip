@@ -21,9 +21,6 @@ namespace ms {
 
 constexpr int DBN = 64, DBK = 64, DPF = 3;
 
-// s_waitcnt immediate for vmcnt(n) with expcnt/lgkmcnt left alone (gfx9 encoding)
-__host__ __device__ constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
-
 template <int MT, int EPI>
 __global__ __launch_bounds__(256, 2) void dgemm_kernel(const bf16_t* __restrict__ X,
                                                       const bf16_t* __restrict__ W,

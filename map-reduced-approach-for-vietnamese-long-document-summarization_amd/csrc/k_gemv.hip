@@ -58,7 +58,7 @@ constexpr size_t kMaxLds = 160 * 1024;
 // staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of a
 // fragment read on different banks); rows >= M alias row M-1 and are never stored.
 static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
-  size_t xs = xlds ? (size_t)M * (2 * (size_t)K + 16) : 0;
+  size_t xs = xlds ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;  // per-wave partials
   return xs > red ? xs : red;
 }
@@ -82,7 +82,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
   }
 
-  // 1. issue this wave's whole W stream first (HBM latency overlaps the X staging)
+  // 1. X rows by LDS DMA first, then this wave's whole W stream (gemv_dma_x)
+  if constexpr (XL) gemv_dma_x(smem, X, M, K, ldk);
+  __builtin_amdgcn_sched_barrier(0);
   uint4 w[U][NT][2];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
@@ -93,11 +95,12 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       w[u][n][1] = ldw16(wp + u * 64 + 8);
     }
   }
-  // 2. stage the M rows of X into LDS (XL) -- or read fragments from L2 (large M*K)
-  const size_t xstride = 2 * (size_t)K + 16;
+  // 2. the X image has landed once at most the W loads are pending -- or X fragments are
+  // read from L2 (large M*K)
   if constexpr (XL) {
-    gemv_stage_x(smem, X, M, K, ldk);
-    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
+    __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the W loads too
   }
 
   f32x4 acc[MT][NT];
@@ -112,9 +115,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       const int xrow = min(m * 16 + fr, M - 1);
       bf16x8 x0, x1;
       if constexpr (XL) {
-        const char* xr = smem + xrow * xstride + (kbeg + u * 64 + 16 * fg) * 2;
-        x0 = *(const bf16x8*)xr;
-        x1 = *(const bf16x8*)(xr + 16);
+        const int k0 = kbeg + u * 64 + 16 * fg;
+        x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
+        x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
       } else {
         const bf16_t* xg = X + (size_t)xrow * ldk + kbeg + u * 64 + 16 * fg;
         x0 = as_bf16x8(ldg16(xg));

@@ -203,7 +203,6 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
   if (qm.n > 1 && n0 >= qm.row0_1) { type = qm.type1; row_bytes = qm.row_bytes1; rbase = n0 - qm.row0_1; base = qm.base1; }
   if (qm.n > 2 && n0 >= qm.row0_2) { type = qm.type2; row_bytes = qm.row_bytes2; rbase = n0 - qm.row0_2; base = qm.base2; }
   const int sb0 = wave * SBW;
-  const size_t xstride = 2 * (size_t)K + 16;
 
   f32x4 acc[MT][NT];
 #pragma unroll
@@ -211,6 +210,9 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // X rows by LDS DMA first (gemv_dma_x), then the weight stream
+  if constexpr (XL) gemv_dma_x(smem, X, M, K, ldx);
+  __builtin_amdgcn_sched_barrier(0);
   if (type == MS_QT_Q4_K) {
     uint4 hq[SBW][NT], q0[SBW][NT], q1[SBW][NT];
 #pragma unroll
@@ -222,21 +224,22 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         q0[j][n] = ldw16(bp + 16 + 32 * g);
         q1[j][n] = ldw16(bp + 32 + 32 * g);
       }
-    if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K, ldx);
-      __syncthreads();
+    if constexpr (XL) {  // the X image has landed once at most the weight loads are pending
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * SBW * NT));
+      __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the weight loads too
     }
     // X_s: the sum of each row's x over each 32-weight sub-block of this block's K range,
     // [sub-block][16*MT rows] fp32 after the X image (rows >= M: 0), fixed summation order
     const int nsub = K / 32;
-    float* xsum = (float*)(smem + (XL ? (size_t)M * xstride : 0));
+    float* xsum = (float*)(smem + (XL ? gemv_x_lds_bytes(M, K) : 0));
     for (int e = threadIdx.x; e < nsub * 16 * MT; e += blockDim.x) {
       const int sidx = e / (16 * MT), r = e - sidx * (16 * MT);
       float a = 0.f;
       if (r < M) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const bf16x8 v = XL ? *(const bf16x8*)(smem + r * xstride + (sidx * 32 + 8 * c) * 2)
+          const bf16x8 v = XL ? *(const bf16x8*)(smem + x_lds(r, sidx * 32 + 8 * c, K))
                               : *(const bf16x8*)(X + (size_t)r * ldx + sidx * 32 + 8 * c);
 #pragma unroll
           for (int i = 0; i < 8; ++i) a += (float)v[i];
@@ -277,7 +280,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
+            const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
                                  : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
             const f32x4 A = mfma16(xf, wf, f32x4{0.f, 0.f, 0.f, 0.f});
             const f32x4 xs = *(const f32x4*)(xsum + ks * 16 * MT + m * 16 + 4 * g);
@@ -301,9 +304,10 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         sc[j][n] = ldw16(bp + 192);
         dw[j][n] = *(const uint32_t*)(bp + 208);
       }
-    if constexpr (XL) {  // X rows -> LDS once per block; else fragments straight from L2 (large M*K)
-      gemv_stage_x(smem, X, M, K, ldx);
-      __syncthreads();
+    if constexpr (XL) {  // the X image has landed once at most the weight loads are pending
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(5 * SBW * NT));
+      __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the weight loads too
     }
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
@@ -334,7 +338,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = XL ? *(const bf16x8*)(smem + xrow * xstride + k * 2)
+            const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
                                  : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
@@ -365,12 +369,12 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
 static constexpr size_t kLdsCap = 160 * 1024;
 
 static bool qx_in_lds(int M, int K) {
-  return (size_t)M * (2 * (size_t)K + 16) + (size_t)(K / 32) * 16 * ((M + 15) / 16) * 4 <= kLdsCap;
+  return gemv_x_lds_bytes(M, K) + (size_t)(K / 32) * 16 * ((M + 15) / 16) * 4 <= kLdsCap;
 }
 
 static size_t qlds(const QPlan& p, int M, int K) {
   // X image (when it fits) + the Q4_K sub-block sums [K/32][16*MT] fp32
-  const size_t xs = (qx_in_lds(M, K) ? (size_t)M * (2 * (size_t)K + 16) : 0) + (size_t)(K / 32) * 16 * p.MT * 4;
+  const size_t xs = (qx_in_lds(M, K) ? gemv_x_lds_bytes(M, K) : 0) + (size_t)(K / 32) * 16 * p.MT * 4;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }

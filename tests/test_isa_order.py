@@ -1,0 +1,89 @@
+"""Instruction-order guard for the decode GEMVs' X staging (CPU: reads the built library).
+
+k_gemv.hip / k_qgemv.hip copy X into LDS by DMA (global_load_lds) BEFORE issuing the
+weight stream, then wait ``vmcnt(<number of weight loads>)`` and pass a fence-free barrier
+(gemv_common.h gemv_dma_x).  That wait is only correct if the compiler kept every weight
+load after the last DMA: vmcnt retires in issue order, so a weight load hoisted above the
+DMA would let the barrier pass with the X image still in flight.  This test disassembles
+the gfx950 code objects inside libmapsum.so and checks, for every LDS-staged GEMV
+instance, that no DMA follows a weight load before the barrier, and that the explicit wait
+in front of that barrier leaves no more loads outstanding than were issued after the DMA.
+"""
+import os
+import re
+import shutil
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "map-reduced-approach-for-vietnamese-long-document-summarization_amd", "mapsum",
+                   "libmapsum.so")
+LLVM = "/opt/rocm/lib/llvm/bin"
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _code_objects(path):
+    """gfx950 ELF code objects of every offload bundle in the library's .hip_fatbin."""
+    tmp = path + ".fatbin.tmp"
+    subprocess.run([os.path.join(LLVM, "llvm-objcopy"), "--dump-section=.hip_fatbin=" + tmp, path, "/dev/null"],
+                   check=True, capture_output=True)
+    data = open(tmp, "rb").read()
+    os.remove(tmp)
+    out = []
+    pos = data.find(MAGIC)
+    while pos >= 0:
+        n = int.from_bytes(data[pos + 24:pos + 32], "little")
+        q = pos + 32
+        for _ in range(n):
+            off, size, tlen = (int.from_bytes(data[q + 8 * i:q + 8 * i + 8], "little") for i in range(3))
+            triple = data[q + 24:q + 24 + tlen].decode()
+            q += 24 + tlen
+            if "gfx950" in triple and size:
+                out.append(data[pos + off:pos + off + size])
+        pos = data.find(MAGIC, pos + 32)
+    return out
+
+
+def _functions(elf_bytes, tmpdir):
+    p = os.path.join(tmpdir, "co.elf")
+    open(p, "wb").write(elf_bytes)
+    txt = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", p],
+                         check=True, capture_output=True, text=True).stdout
+    funcs, cur = {}, None
+    for line in txt.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(.+)>:$", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+        elif cur is not None and line.strip():
+            funcs[cur].append(line.strip())
+    return funcs
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and shutil.which(os.path.join(LLVM, "llvm-objdump"))),
+                    reason="libmapsum.so not built or no llvm-objdump")
+def test_gemv_x_dma_precedes_weight_stream(tmp_path):
+    checked = 0
+    for co in _code_objects(LIB):
+        for name, ins in _functions(co, str(tmp_path)).items():
+            # LDS-staged instances only: gemv_kernel<..., XL=true>, qgemv_kernel<..., XL=true>
+            if not re.search(r"q?gemv_kernelI.*Lb1EEEv", name):
+                continue
+            ops = [i.split()[0] for i in ins]
+            bar = [k for k, o in enumerate(ops) if o == "s_barrier"]
+            assert bar, name
+            first = bar[0]
+            dma = [k for k in range(first) if ops[k].startswith("global_load_lds")]
+            wl = [k for k in range(first) if ops[k].startswith("global_load") and not ops[k].startswith("global_load_lds")]
+            assert dma and wl, name
+            assert max(dma) < min(wl), f"{name}: a weight load was scheduled above the X DMA"
+            # the explicit wait in front of the barrier: vmcnt(N) with N <= loads issued after the DMA
+            w = [k for k in range(max(dma), first) if ops[k] == "s_waitcnt" and "vmcnt" in ins[k]]
+            assert w, f"{name}: no vmcnt wait between the X DMA and the barrier"
+            n = int(re.search(r"vmcnt\((\d+)\)", ins[w[-1]]).group(1))
+            after = sum(1 for k in range(max(dma), w[-1]) if ops[k].startswith("global_load")
+                        and not ops[k].startswith("global_load_lds"))
+            assert n <= after, f"{name}: vmcnt({n}) but only {after} weight loads after the DMA"
+            checked += 1
+    assert checked >= 8, checked
