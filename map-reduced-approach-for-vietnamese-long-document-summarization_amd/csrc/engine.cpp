@@ -113,10 +113,13 @@ struct ms_engine {
   float* slabs = nullptr;
   int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
   // large-batch regime (B >= dgemm_min rows in flight, BASELINE configs[2]): QKV / O / down /
-  // lm_head on the skinny GEMM (k_dgemm.hip, split 6 / 6 / 8 / 1), gate/up on the 128x128
-  // GEMM.  Each regime is batch-invariant on its own (no kernel choice inside it depends on
-  // B); between the regimes a row's summation order differs.
-  int dgemm_min = 49, dsplit_qkv = 6, dsplit_o = 6, dsplit_down = 8;
+  // lm_head on the skinny GEMM (k_dgemm.hip, split 6 / 4 / 8 / 1), gate/up on it too up to
+  // 128 rows and on the 128x128 GEMM above.  The regimes B < 24, 24..128 and > 128 are each
+  // batch-invariant (no kernel or split choice inside one depends on B); between them a
+  // row's summation order differs.  The crossover: at M = 16 the GEMV and the skinny GEMM
+  // tie over a layer's four projections, at M = 32 the skinny GEMM takes 30 % less
+  // (profiles/r02/v7_dgemm_lds_sync_ab.txt).
+  int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large(int B) const { return B >= dgemm_min; }
   int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
@@ -295,8 +298,13 @@ struct ms_engine {
     pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
     residual_norm(Ly.ffn_norm, B);
     if (large(B)) {
+      // gate/up + SwiGLU: the skinny GEMM up to 128 rows (41 vs 55 us at M = 128,
+      // profiles/r02/v7_dgemm_lds_sync_ab.txt), the 128x128 GEMM above (one block per CU)
       prof_begin(K_GEMV);
-      launch_gemm(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_EPI_SWIGLU, stream);
+      if (B <= 128 && dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU))
+        launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream);
+      else
+        launch_gemm(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_EPI_SWIGLU, stream);
       prof_end(K_GEMV);
     } else {
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);

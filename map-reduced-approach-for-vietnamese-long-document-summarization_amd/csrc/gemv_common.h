@@ -21,6 +21,15 @@ __device__ __forceinline__ uint4 ldw16(const void* p) {
 // s_waitcnt immediate for vmcnt(n) with expcnt/lgkmcnt left alone (gfx9 encoding)
 __host__ __device__ constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
 
+// __syncthreads() for LDS only: waits for this wave's LDS operations (lgkmcnt) but not for
+// its global loads, so a register-staged weight stream stays in flight across the barrier
+// (a full __syncthreads() fence drains vmcnt as well).  Not for LDS written by DMA.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // X rows [M][K] bf16 (row stride ldx elements) -> LDS image of M rows x 2K bytes, 16-B
 // chunk c of row r stored at chunk c ^ (r & 7) (the rows of an MFMA fragment read land on
 // different bank groups).  Copied by LDS DMA (global_load_lds, 1 KiB per wave instruction)

@@ -6,11 +6,12 @@
 // GEMV (k_gemv.hip) owns 16 weight rows per block and re-reads all M x K activations per
 // block: at M = 64 the gate/up launch reads 4x more X from L2 than W from HBM and stalls on
 // L2.  Here a block owns 64 weight rows (4 waves x 16) and ALL M rows:
-//  * X (M x 64 per K step) goes HBM/L2 -> LDS by global_load_lds (1 KiB per wave
-//    instruction, source-side XOR swizzle chunk ^ (row & 7): conflict-free ds_read_b128),
-//    double-buffered; the 4 waves share it, so X is read from L2 once per 64 weight rows;
-//  * W streams straight to VGPRs, each wave its own 16 rows, PF K steps in flight
-//    (32 contiguous bytes per lane per step, as in the GEMV);
+//  * X (M x 64 per K step) is register-staged one step ahead into a double-buffered LDS
+//    image (XOR swizzle chunk ^ (row & 7): conflict-free ds_read_b128); the 4 waves share
+//    it, so X is read from L2 once per 64 weight rows;
+//  * W streams straight to VGPRs, each wave its own 16 rows, DPF K steps in flight
+//    (32 contiguous bytes per lane per step, as in the GEMV), and stays in flight across
+//    the step's LDS-only barrier (an LDS-DMA X image would force a full vmcnt drain there);
 //  * v_mfma_f32_16x16x32_bf16, the wave's 16 weight rows as MFMA columns, MT m-tiles;
 //  * split-K over gridDim.y for the narrow projections (fp32 slabs, folded by the next
 //    residual_rmsnorm / attention prologue exactly like the GEMV's).
@@ -19,79 +20,95 @@
 
 namespace ms {
 
-constexpr int DBN = 64, DBK = 64, DPF = 3;
+constexpr int DBN = 64, DBK = 64;
+
+// W ring depth: 3 K steps in flight at 2 blocks per CU; M > 128 (MT = 16) needs more
+// registers than 2 blocks per CU allow, so 1 block per CU with a deeper ring
+template <int MT> constexpr int dgemm_dpf() { return MT >= 16 ? 6 : 3; }
 
 template <int MT, int EPI>
-__global__ __launch_bounds__(256, 2) void dgemm_kernel(const bf16_t* __restrict__ X,
+__global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16_t* __restrict__ X,
                                                       const bf16_t* __restrict__ W,
                                                       void* __restrict__ out, int M, int N, int K,
                                                       int ldk, int ldo) {
-  constexpr int XB = 16 * MT * DBK * 2;  // one X stage: 16*MT rows x 128 B
+  constexpr int DPF = dgemm_dpf<MT>();
+  // one X stage: XR rows x 128 B (16*MT rounded up to whole 16-B chunks per thread)
+  constexpr int XR = 16 * MT < 32 ? 32 : 16 * MT;
+  constexpr int XB = XR * DBK * 2;
+  constexpr int XI = XR * 8 / 256;  // 16-B chunks of one stage per thread
   __shared__ __attribute__((aligned(16))) char smem[2 * XB > 4 * MT * 256 * 4 ? 2 * XB : 4 * MT * 256 * 4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int n0 = blockIdx.x * DBN;
   const int kb = blockIdx.y * K;  // this split's K range in rows of length ldk
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) out = (float*)out + (size_t)blockIdx.y * M * ldo;
+  const int nk = K / DBK;
 
-  // X DMA: instruction i of a stage covers rows 4*(wave*MT/2... ) -- rows r = i*32 + tid/8,
-  // chunk c = tid&7 written at LDS row r, chunk c, from global chunk c ^ (r & 7)
-  constexpr int XI = (16 * MT * 8 + 255) / 256;  // 16-B DMA pieces per thread per stage
-  auto stage_x = [&](int buf, int k0) {
+  // X is register-staged one K step ahead: chunk c = tid + 256 i of a stage is row c/8,
+  // 16-B chunk c%8, stored at chunk (c%8) ^ (row & 7) (conflict-free fragment reads).
+  // Every wait is then a register dependency the compiler counts itself, and the one
+  // barrier per step is LDS-only (lds_sync): the weight loads stay in flight across it.
+  uint4 xr[XI];
+  auto load_x = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int r = i * 32 + (tid >> 3);
-      if (r < 16 * MT) {
-        const int gc = (tid & 7) ^ (r & 7);
-        const bf16_t* src = X + (size_t)min(r, M - 1) * ldk + kb + k0 + gc * 8;
-        char* dst = smem + buf * XB + (i * 32 + (wave << 3)) * 128;  // wave's 8 rows of piece i
-        __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)dst, 16, 0, 0);
-      }
+      const int c = tid + 256 * i, r = c >> 3;
+      xr[i] = ldg16(X + (size_t)min(r, M - 1) * ldk + kb + k0 + (c & 7) * 8);
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int c = tid + 256 * i, r = c >> 3;
+      *(uint4*)(smem + buf * XB + r * 128 + (((c & 7) ^ (r & 7)) << 4)) = xr[i];
     }
   };
   // W: lane (fr, fg) holds k0 + 16 fg .. +15 of row n0 + 16 wave + fr (32 contiguous bytes),
-  // a DPF-slot register ring; X: the same permuted k order from the LDS image
+  // a DPF-slot register ring, DPF K steps in flight; X: the same permuted k order from LDS
   const bf16_t* wrow = W + (size_t)min(n0 + 16 * wave + fr, N - 1) * ldk + kb + 16 * fg;
   uint4 wr[DPF][2];
-  const int nk = K / DBK;
+  load_x(0);
+  store_x(0);
+  load_x(min(1, nk - 1) * DBK);
 #pragma unroll
-  for (int p = 0; p < DPF - 1; ++p)
-    if (p < nk) {
-      wr[p][0] = ldw16(wrow + p * DBK);
-      wr[p][1] = ldw16(wrow + p * DBK + 8);
-    }
-  stage_x(0, 0);
+  for (int p = 0; p < DPF; ++p) {
+    wr[p][0] = ldw16(wrow + min(p, nk - 1) * DBK);
+    wr[p][1] = ldw16(wrow + min(p, nk - 1) * DBK + 8);
+  }
+  lds_sync();
 
   f32x4 acc[MT];
 #pragma unroll
   for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    // issue order per step: W(t+DPF-1) into the slot step t-1 consumed, then X(t+1); vmcnt is
-    // in order, so X(t) -- and every older W, W(t) included -- has landed once at most the
-    // ops issued after it are pending
-    const bool wmore = t + DPF - 1 < nk, more = t + 1 < nk;
-    if (wmore) {
-      wr[(t + DPF - 1) % DPF][0] = ldw16(wrow + (t + DPF - 1) * DBK);
-      wr[(t + DPF - 1) % DPF][1] = ldw16(wrow + (t + DPF - 1) * DBK + 8);
-    }
-    if (more) stage_x(buf ^ 1, (t + 1) * DBK);
-    if (wmore) __builtin_amdgcn_s_waitcnt(vmcnt_imm(2 + XI));
-    else if (more) __builtin_amdgcn_s_waitcnt(vmcnt_imm(XI));
-    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    __syncthreads();
-    const uint4 w0 = wr[t % DPF][0], w1 = wr[t % DPF][1];
-    const char* xs = smem + buf * XB;
+  // unrolled by DPF so every ring slot is a compile-time register set (a runtime-indexed
+  // ring compiles to selects that wait for each load as soon as it is issued); past the
+  // end the loads are clamped re-reads, never branched around
+  for (int t0 = 0; t0 < nk; t0 += DPF) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m) {
-      const int row = m * 16 + fr;
-      const bf16x8 x0 = *(const bf16x8*)(xs + row * 128 + (((2 * fg) ^ (row & 7)) << 4));
-      const bf16x8 x1 = *(const bf16x8*)(xs + row * 128 + (((2 * fg + 1) ^ (row & 7)) << 4));
-      acc[m] = mfma16(x0, as_bf16x8(w0), acc[m]);
-      acc[m] = mfma16(x1, as_bf16x8(w1), acc[m]);
+    for (int i = 0; i < DPF; ++i) {
+      const int t = t0 + i;
+      if (t >= nk) break;  // block-uniform
+      const int buf = t & 1;
+      // (a) X(t) x W(t)
+      const char* xs = smem + buf * XB;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const int row = m * 16 + fr;
+        const bf16x8 x0 = *(const bf16x8*)(xs + row * 128 + (((2 * fg) ^ (row & 7)) << 4));
+        const bf16x8 x1 = *(const bf16x8*)(xs + row * 128 + (((2 * fg + 1) ^ (row & 7)) << 4));
+        acc[m] = mfma16(x0, as_bf16x8(wr[i][0]), acc[m]);
+        acc[m] = mfma16(x1, as_bf16x8(wr[i][1]), acc[m]);
+      }
+      // (b) X(t+1) into the other stage (every wave finished reading it before the last sync)
+      store_x(buf ^ 1);
+      // (c) X(t+2) and W(t+DPF) (into the slot just consumed) in flight
+      load_x(min(t + 2, nk - 1) * DBK);
+      wr[i][0] = ldw16(wrow + min(t + DPF, nk - 1) * DBK);
+      wr[i][1] = ldw16(wrow + min(t + DPF, nk - 1) * DBK + 8);
+      // (d) X(t+1) visible; every wave done with stage buf before X(t+2) overwrites it
+      lds_sync();
     }
-    __syncthreads();  // every wave is done with buf before X(t+2) overwrites it
   }
 
   // epilogue: acc[m][j] = C[row m*16 + 4 fg + j][col n0 + 16 wave + fr]

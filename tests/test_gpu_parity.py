@@ -384,16 +384,18 @@ def test_batch_invariance(eng):
         assert alone.ids == r.ids
 
 
-def test_batch_invariance_large_regime(dev):
-    """Within the large-batch regime (B >= 49 rows in flight) a chunk's summary does not
-    depend on its companions either: the first 60 of 100 chunks alone == in the batch."""
-    e = Engine(TINY, device=0, max_batch=100, max_ctx=256, max_prefill_tokens=16384)
+@pytest.mark.parametrize("n_all,n_sub", [(100, 60), (200, 140)])
+def test_batch_invariance_large_regime(dev, n_all, n_sub):
+    """Within each large-batch regime (24..128 rows in flight: skinny GEMM everywhere;
+    > 128: gate/up on the 128x128 GEMM) a chunk's summary does not depend on its
+    companions either: the first n_sub of n_all chunks alone == in the batch."""
+    e = Engine(TINY, device=0, max_batch=n_all, max_ctx=256, max_prefill_tokens=32768)
     try:
         e.init_synthetic(SEED, STD, JITTER)
-        prompts = [_prompt(20 + (11 * i) % 100, 1300 + i) for i in range(100)]
+        prompts = [_prompt(20 + (11 * i) % 100, 1300 + i) for i in range(n_all)]
         together = e.generate(prompts, num_predict=10, ignore_eos=True)
-        alone = e.generate(prompts[:60], num_predict=10, ignore_eos=True)
-        assert [r.ids for r in alone] == [r.ids for r in together[:60]]
+        alone = e.generate(prompts[:n_sub], num_predict=10, ignore_eos=True)
+        assert [r.ids for r in alone] == [r.ids for r in together[:n_sub]]
     finally:
         e.close()
 
@@ -470,10 +472,10 @@ def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
 
 @pytest.mark.parametrize("nb", [20, 50, 70, 130])
 def test_decode_paths_larger_batch(oracle, nb):
-    """B = 20 runs the weight-streaming GEMVs with MT = 2 tiles; B >= 49 the large-batch
-    regime (skinny GEMM k_dgemm.hip for QKV / O / down / lm_head with split-K slabs, the
-    128x128 GEMM for gate/up).  All must agree with the oracle (teacher-forced, flips only
-    at near-ties)."""
+    """B = 20 runs the weight-streaming GEMVs with MT = 2 tiles; B >= 24 the large-batch
+    regime (skinny GEMM k_dgemm.hip for QKV / O / down / lm_head with split-K slabs, and for
+    gate/up up to 128 rows; the 128x128 GEMM for gate/up above).  All must agree with the
+    oracle (teacher-forced, flips only at near-ties)."""
     e = Engine(TINY, device=0, max_batch=nb, max_ctx=256, max_prefill_tokens=8192)
     try:
         e.init_synthetic(SEED, STD, JITTER)
