@@ -112,15 +112,16 @@ struct ms_engine {
   // residual by the next residual_rmsnorm launch (pending_split = S of the unfolded slabs)
   float* slabs = nullptr;
   int split_qkv = 6, split_o = 6, split_down = 4, pending_split = 0;
-  // large-batch regime (B >= dgemm_min rows in flight, BASELINE configs[2]): QKV / O / down /
-  // lm_head on the skinny GEMM (k_dgemm.hip, split 6 / 4 / 8 / 1), gate/up on it too up to
-  // 128 rows and on the 128x128 GEMM above.  The regimes B < 24, 24..128 and > 128 are each
-  // batch-invariant (no kernel or split choice inside one depends on B); between them a
-  // row's summation order differs.  The crossover: at M = 16 the GEMV and the skinny GEMM
-  // tie over a layer's four projections, at M = 32 the skinny GEMM takes 30 % less
-  // (profiles/r02/v7_dgemm_lds_sync_ab.txt).
+  // large-batch regime (BASELINE configs[2]): QKV / O / down / gate-up / lm_head on the skinny
+  // GEMM (k_dgemm.hip, split 6 / 4 / 8 / 1 / 1).  The regime is chosen per ENGINE, from its
+  // max_batch (>= dgemm_min), never from the rows of one step: every step of an engine then
+  // runs one arithmetic whatever the number of sequences in flight (admission ramps, tails,
+  // a chunk alone), so a chunk's summary never depends on its companions.  The crossover:
+  // at M = 16 the GEMV and the skinny GEMM tie over a layer's four projections, at M = 32
+  // the skinny GEMM takes 30 % less (profiles/r02/v7_dgemm_lds_sync_ab.txt).
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
-  bool large(int B) const { return B >= dgemm_min; }
+  bool large_engine = false;
+  bool large(int) const { return large_engine; }
   int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
   // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
@@ -226,7 +227,8 @@ struct ms_engine {
       return B <= kMaxSlabRows && attn_slabs && residual_rmsnorm_supported(kMaxSplit, H) &&
              dgemm_supported(B, QKVN, H, dsplit_qkv, MS_GEMV_EPI_STORE_F32) &&
              dgemm_supported(B, H, Hq * D, dsplit_o, MS_GEMV_EPI_STORE_F32) &&
-             dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32) && (2 * F) % 32 == 0 &&
+             dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32) &&
+             dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU) && (2 * F) % 32 == 0 &&
              attn_decode_supported(B, Hq, Hk, max_pages * kPage);
     return B <= kMaxGemvRows && residual_rmsnorm_supported(kMaxSplit, H) &&
            (attn_slabs ? gemv_split_supported(B, QKVN, H, 1) : gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
@@ -298,13 +300,10 @@ struct ms_engine {
     pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
     residual_norm(Ly.ffn_norm, B);
     if (large(B)) {
-      // gate/up + SwiGLU: the skinny GEMM up to 128 rows (41 vs 55 us at M = 128,
-      // profiles/r02/v7_dgemm_lds_sync_ab.txt), the 128x128 GEMM above (one block per CU)
+      // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
+      // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
       prof_begin(K_GEMV);
-      if (B <= 128 && dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU))
-        launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream);
-      else
-        launch_gemm(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_EPI_SWIGLU, stream);
+      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream);
       prof_end(K_GEMV);
     } else {
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
@@ -542,6 +541,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_SPLIT_O")) E.split_o = atoi(v);
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
+    E.large_engine = cfg->max_batch >= E.dgemm_min;
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);

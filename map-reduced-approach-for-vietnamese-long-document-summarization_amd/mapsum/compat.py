@@ -162,10 +162,10 @@ def _default_factory(model_name: str) -> MapBackend:
     d = os.environ.get("MAPSUM_MODEL_DIR")
     if not d:
         raise RuntimeError(f"no backend registered for model {model_name!r} and MAPSUM_MODEL_DIR unset")
-    # 23 in flight keeps every decode step in the GEMV regime (engine.cpp dgemm_min = 24), so
-    # a batched call returns exactly what it returns alone (batch invariance)
+    # the decode regime is fixed per engine, so any max_batch keeps a batched
+    # call equal to the same call alone; 64 in flight runs the large-batch regime
     eng = Engine(LLAMA32_3B, device=int(os.environ.get("LOCAL_RANK", 0)),
-                 max_batch=int(os.environ.get("MAPSUM_MAX_BATCH", 23)),
+                 max_batch=int(os.environ.get("MAPSUM_MAX_BATCH", 64)),
                  max_ctx=int(os.environ.get("MAPSUM_MAX_CTX", 16384)),
                  max_prefill_tokens=int(os.environ.get("MAPSUM_MAX_PREFILL", 32768)))
     load_hf_dir(eng, d)

@@ -11,9 +11,9 @@ Follows runners/run_summarization_ollama_mapreduce_hierarchical.py:
 The reference awaits every target, and every chunk inside a target, one after another
 (:151-160, :232-256).  All of them are independent, so here one depth is one batch: every
 map prompt of every target at that depth is issued together, then every reduce prompt.
-The engine is greedy and batch-invariant within a decode regime (at most 23
-sequences in flight, the default engine's max_batch), so each call returns the string it
-would have returned alone, and the tree ends up identical.
+The engine is greedy and batch-invariant (one decode arithmetic per engine,
+whatever the number of sequences in flight), so each call returns the string it would have
+returned alone, and the tree ends up identical.
 """
 from __future__ import annotations
 

@@ -13,7 +13,6 @@ Mirrors the LangGraph in runners/run_summarization_ollama_mapreduce.py:75-181 (S
 Differences that do not change any string the reference produces:
 - The reference awaits collapse groups one after another (:134-135).  Each group's
   reduce call depends only on its own group, and the engine is greedy and batch-invariant
-  within a decode regime (<= 23 in flight, the default max_batch)
   (DESIGN.md §5), so the groups are issued together and land in one batch.
 - ``acollapse_docs`` also merges Document metadata; the map path carries none, so only
   the page_content survives here.

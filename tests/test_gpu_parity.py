@@ -384,11 +384,12 @@ def test_batch_invariance(eng):
         assert alone.ids == r.ids
 
 
-@pytest.mark.parametrize("n_all,n_sub", [(100, 60), (200, 140)])
+@pytest.mark.parametrize("n_all,n_sub", [(100, 60), (200, 1)])
 def test_batch_invariance_large_regime(dev, n_all, n_sub):
-    """Within each large-batch regime (24..128 rows in flight: skinny GEMM everywhere;
-    > 128: gate/up on the 128x128 GEMM) a chunk's summary does not depend on its
-    companions either: the first n_sub of n_all chunks alone == in the batch."""
+    """An engine with max_batch >= 24 runs every decode step in the large-batch regime
+    (skinny GEMM, engine.cpp large_engine), however many sequences are in flight, so a
+    chunk's summary does not depend on its companions either: the first n_sub of n_all
+    chunks (one chunk alone included) == in the batch."""
     e = Engine(TINY, device=0, max_batch=n_all, max_ctx=256, max_prefill_tokens=32768)
     try:
         e.init_synthetic(SEED, STD, JITTER)
