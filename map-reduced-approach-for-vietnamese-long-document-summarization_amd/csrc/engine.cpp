@@ -121,6 +121,7 @@ struct ms_engine {
   // the skinny GEMM takes 30 % less (profiles/r02/v7_dgemm_lds_sync_ab.txt).
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
+  int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
   bool large(int) const { return large_engine; }
   int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
@@ -542,6 +543,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
+    E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
@@ -1055,6 +1057,7 @@ static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int3
   da.B = B;
   // the split grid only depends on the longest sequence rounded up to 256 keys
   da.max_len = ((max_len + 255) / 256) * 256;
+  da.ppw = E.attn_ppw;
   if (E.use_graphs && E.prof_mask == 0) {
     const auto key = std::make_pair(B, da.max_len);
     auto it = E.decode_graphs.find(key);

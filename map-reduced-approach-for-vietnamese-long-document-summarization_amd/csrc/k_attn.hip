@@ -16,6 +16,8 @@
 // 16+4g..16+4g+3 for lane group g), identically on both operands.
 // LDS images: K rows swizzled chunk ^ (row & 15) (ds_read_b128, conflict-free);
 // V rows swizzled chunk ^ ((row & 7) << 1) (tr reads conflict-free).
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace ms {
@@ -271,15 +273,39 @@ constexpr int kSplitPages = 4;  // = waves per block
 constexpr int kMaxGroup = 8;    // q heads per kv head
 constexpr int kMaxSlabs = 8;    // QKV split-K slabs (engine kMaxSplit)
 
-// pages per wave: 2 halves the block count (one resident round instead of 1.1 at B = 8,
-// 2304 keys), the second page's loads issued under the first page's math (MS_ATTN_PPW)
-static int decode_ppw() {
-  static const int v = [] { const char* e = getenv("MS_ATTN_PPW"); return e ? atoi(e) : 2; }();
-  return v == 1 ? 1 : 2;
+// Pages per wave (ppw) and splits per (sequence, kv head).  Every wave walks its pages with
+// the next page's K and V in flight under the current page's math, so more pages per wave
+// cost nothing but parallelism.  ppw is fixed per ENGINE from its max_batch and max_ctx
+// (the split boundaries, at multiples of 4*ppw pages, set a sequence's summation order, so
+// they must not move with the batch): ~2 blocks per CU in one round (512 blocks) at a full
+// batch of max_ctx keys, at least 2 pages per wave.  B = 8 at 2304 keys -> ppw 2, 5 splits,
+// 320 blocks; B = 128 -> ppw 16, 1 split, 1024 blocks: the per-block prologue (QKV slab
+// fold, RoPE) and epilogue (merge, partial) are paid once per 36 pages instead of per 8.
+// MS_ATTN_PPW pins ppw (tuning).
+constexpr int kTargetBlocks = 512, kMaxPPW = 16;
+static int decode_ppw_env() {
+  static const int v = [] { const char* e = getenv("MS_ATTN_PPW"); return e ? atoi(e) : 0; }();
+  return v;
 }
-static int decode_nsplit(int max_len) {
-  const int per = kSplitPages * kPage * decode_ppw();
-  return (max_len + per - 1) / per;
+int attn_decode_ppw(int max_batch, int Hk, int max_ctx) {
+  const int np = (max_ctx + kPage - 1) / kPage;
+  int ppw = decode_ppw_env();
+  if (ppw <= 0) {
+    const long want = ((long)np * max_batch * Hk + (long)kSplitPages * kTargetBlocks - 1) /
+                      ((long)kSplitPages * kTargetBlocks);
+    ppw = (int)std::max(2L, std::min((long)kMaxPPW, want));
+  }
+  return std::max(1, std::min(ppw, kMaxPPW));
+}
+static int decode_nsplit(int ppw, int max_len) {
+  const int np = (max_len + kPage - 1) / kPage;
+  return (np + kSplitPages * ppw - 1) / (kSplitPages * ppw);
+}
+// the most splits any B can get (ppw >= 1 under MS_ATTN_PPW, else >= 2)
+static int decode_nsplit_max(int max_len) {
+  const int np = (max_len + kPage - 1) / kPage;
+  const int ppw_min = decode_ppw_env() > 0 ? 1 : 2;
+  return (np + kSplitPages * ppw_min - 1) / (kSplitPages * ppw_min);
 }
 
 constexpr int kMaxTickets = 4096;  // (b, kv head) pairs per launch
@@ -288,22 +314,23 @@ constexpr int kMaxSplits = 127;
 // workspace: [tickets: kMaxTickets u32, zero at allocation, reset by each last arriver]
 //            [partials: (b, q head, split) x 132 floats]
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
-  return (size_t)kMaxTickets * 4 + (size_t)B * Hq * decode_nsplit(max_len) * 132 * sizeof(float);
+  return (size_t)kMaxTickets * 4 + (size_t)B * Hq * decode_nsplit_max(max_len) * 132 * sizeof(float);
 }
 
 size_t attn_decode_ticket_bytes() { return (size_t)kMaxTickets * 4; }
 
 bool attn_decode_supported(int B, int Hq, int Hk, int max_len) {
   return Hk >= 1 && Hq % Hk == 0 && Hq / Hk <= kMaxGroup && B * Hk <= kMaxTickets &&
-         decode_nsplit(max_len) <= kMaxSplits;
+         decode_nsplit_max(max_len) <= kMaxSplits;
 }
 
-template <bool FROM_SLABS, bool FUSED_COMBINE, int PPW>
+// PPWT = 2: the page loop unrolled for exactly 2 pages per wave (the B = 8 plan); 0: runtime
+template <bool FROM_SLABS, bool FUSED_COMBINE, int PPWT>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
                                                           DecodeAttnArgs a, float* __restrict__ ws,
                                                           unsigned* __restrict__ tickets,
                                                           bf16_t* __restrict__ out, int nsplit,
-                                                          float scale_log2) {
+                                                          int ppw, float scale_log2) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + (kMaxGroup + 2) * kHeadDim * 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
@@ -313,8 +340,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   const int slot = a.seq_slot[b];
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
   char* vs_ = smem + wave * 16384;
-  // this wave's pages: pp-th = split*4*PPW + pp*4 + wave (interleaved: waves stay balanced)
-  const int pg0 = split * kSplitPages * PPW + wave;
+  // this wave's pages: split*4*ppw + wave, +4, ... below pend (interleaved: waves stay balanced)
+  const int pg0 = split * kSplitPages * ppw + wave;
+  const int pend = min((split + 1) * kSplitPages * ppw, (len + kPage - 1) / kPage);
   const int pos = len - 1;               // the new token
   bf16_t* qn = (bf16_t*)(smem + 4 * 16384);  // [G][128] roped q
   bf16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
@@ -338,13 +366,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       vr[i] = ld_stream(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
   };
   // issue the first page first, so its HBM latency overlaps the q/k/v prologue
-  if (pg0 * kPage < len) {
+  if (pg0 < pend) {
     fetch_k(pg0);
     fetch_v(pg0);
   }
 
   if constexpr (FROM_SLABS) {
-    const bool owns_new = (pos / kPage) / (kSplitPages * PPW) == split;  // block-uniform
+    const bool owns_new = (pos / kPage) / (kSplitPages * ppw) == split;  // block-uniform
     float* raw = (float*)smem;  // [(G+2)][128] bf16-rounded sums; aliases wave 0's V image
     const size_t sstride = (size_t)a.B * row_stride;
     const float* src = qa.slabs + (size_t)b * row_stride;
@@ -400,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m_run = -INFINITY, l_run = 0.f;
 
-  if (pg0 * kPage < len) {
+  if (pg0 < pend) {
     bf16x8 qf[4];
     {
       const int hl = min(r, G - 1);
@@ -415,10 +443,10 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     }
     const int off = pos % kPage;
 #pragma unroll
-    for (int pp = 0; pp < PPW; ++pp) {
+    for (int pp = 0; PPWT == 0 || pp < PPWT; ++pp) {
       const int pg = pg0 + pp * kSplitPages;
-      if (pg * kPage >= len) break;  // wave-uniform
-      const bool more = pp + 1 < PPW && (pg + kSplitPages) * kPage < len;
+      if (pg >= pend) break;  // wave-uniform
+      const bool more = pg + kSplitPages < pend;
       const bool patch = FROM_SLABS && pg == pos / kPage;  // wave-uniform: holds the new token
       if (patch) {
 #pragma unroll
@@ -615,19 +643,20 @@ void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView
   if (a.B <= 0) return;
   if (!attn_decode_supported(a.B, Hq, Hk, a.max_len)) return;  // callers check
   if (qa.slabs && (qa.S < 1 || qa.S > kMaxSlabs)) return;
-  const int nsplit = decode_nsplit(a.max_len);
+  const int ppw = a.ppw > 0 ? a.ppw : 2;
+  const int nsplit = decode_nsplit(ppw, a.max_len);
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
   unsigned* tickets = (unsigned*)ws;
   ws = (float*)((char*)ws + (size_t)kMaxTickets * 4);
   const dim3 grid(a.B, Hk, nsplit);
-#define AD(SL, FC)                                                                                        \
-  do {                                                                                                     \
-    if (decode_ppw() == 2)                                                                                 \
+#define AD(SL, FC)                                                                                          \
+  do {                                                                                                      \
+    if (ppw == 2)                                                                                           \
       MS_LAUNCH((attn_decode_kernel<SL, FC, 2>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
-                nsplit, scale_log2);                                                                       \
-    else                                                                                                   \
-      MS_LAUNCH((attn_decode_kernel<SL, FC, 1>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
-                nsplit, scale_log2);                                                                       \
+                nsplit, ppw, scale_log2);                                                                   \
+    else                                                                                                    \
+      MS_LAUNCH((attn_decode_kernel<SL, FC, 0>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
+                nsplit, ppw, scale_log2);                                                                   \
   } while (0)
   if (qa.slabs && fused_combine) AD(true, true);
   else if (qa.slabs) AD(true, false);

@@ -28,6 +28,7 @@ struct DecodeAttnArgs {
   const int32_t* seq_slot;  // [B]
   int32_t B;
   int32_t max_len;          // upper bound over the batch (sets the split grid)
+  int32_t ppw;              // pages per wave, fixed per engine (attn_decode_ppw); 0 = 2
 };
 
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
@@ -145,6 +146,9 @@ size_t attn_decode_workspace_bytes(int B, int Hq, int max_len);
 // the split-combine counters at the start of that workspace (zeroed before each step)
 size_t attn_decode_ticket_bytes();
 bool attn_decode_supported(int B, int Hq, int Hk, int max_len);
+// pages per wave of an engine's decode attention (from its max_batch / max_ctx, never from
+// one step's batch: the split boundaries set a sequence's summation order)
+int attn_decode_ppw(int max_batch, int Hk, int max_ctx);
 void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
                         DecodeAttnArgs a, float* ws, hipStream_t s, bool fused_combine = false);
 
