@@ -442,7 +442,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       }
     }
     const int off = pos % kPage;
-#pragma unroll
+    constexpr int kUnrollPages = PPWT > 0 ? PPWT : 1;
+#pragma unroll kUnrollPages
     for (int pp = 0; PPWT == 0 || pp < PPWT; ++pp) {
       const int pg = pg0 + pp * kSplitPages;
       if (pg >= pend) break;  // wave-uniform
