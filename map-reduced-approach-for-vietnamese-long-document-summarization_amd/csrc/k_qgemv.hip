@@ -21,7 +21,8 @@
 //   * Q4_K, one MFMA per 32-weight sub-block: the nibbles become bf16 (128 + q) by a byte
 //     permute against 0x43 (exact integers), the MFMA gives A_s = sum_k x_k (128 + q_k), and
 //     sum_k x_k y_k = d_s A_s - (128 d_s + m_s) X_s with d_s = d*sc_s, m_s = dmin*m_s (ggml's
-//     fp32 d1 / m1) and X_s = sum of the sub-block's x (from LDS) -- 2 FMAs per output
+//     fp32 d1 / m1) and X_s = sum of the sub-block's x (one more MFMA, against ones, shared
+//     by the weight tiles of the block) -- 2 FMAs per output
 //     element per sub-block instead of dequantising every weight: the decode GEMV uses the
 //     exact fp32 dequantised weights (no bf16 rounding of them);
 //   * Q6_K, dequantised in registers to the bf16 values of the bf16 copy.
@@ -229,61 +230,41 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
       __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * SBW * NT));
       __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the weight loads too
     }
-    // X_s: the sum of each row's x over each 32-weight sub-block of this block's K range,
-    // [sub-block][16*MT rows] fp32 after the X image (rows >= M: 0), fixed summation order
-    const int nsub = K / 32;
-    float* xsum = (float*)(smem + (XL ? gemv_x_lds_bytes(M, K) : 0));
-    for (int e = threadIdx.x; e < nsub * 16 * MT; e += blockDim.x) {
-      const int sidx = e / (16 * MT), r = e - sidx * (16 * MT);
-      float a = 0.f;
-      if (r < M) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const bf16x8 v = XL ? *(const bf16x8*)(smem + x_lds(r, sidx * 32 + 8 * c, K))
-                              : *(const bf16x8*)(X + (size_t)r * ldx + sidx * 32 + 8 * c);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) a += (float)v[i];
-        }
-      }
-      xsum[sidx * 16 * MT + r] = a;
-    }
-    __syncthreads();
+    typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+    const bf16x8 ones = __builtin_bit_cast(bf16x8, u4v{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        const uint4 h = hq[j][n];
-        const float d = h2f(h.x), dmin = h2f(h.x >> 16);
-        // get_scale_min_k4 for all 8 sub-blocks at once, one byte each
-        const uint32_t sc03 = h.y & 0x3F3F3F3Fu, m03 = h.z & 0x3F3F3F3Fu;
-        const uint32_t sc47 = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
-        const uint32_t m47 = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
-        const uint32_t qw[8] = {q0[j][n].x, q0[j][n].y, q0[j][n].z, q0[j][n].w,
-                                q1[j][n].x, q1[j][n].y, q1[j][n].z, q1[j][n].w};
+      for (int s_ = 0; s_ < 8; ++s_) {
+        const int k = ((sb0 + j) * 8 + s_) * 32 + 8 * g;  // this lane group's 8 weights
+        const int sh = 8 * (s_ & 3);
 #pragma unroll
-        for (int s_ = 0; s_ < 8; ++s_) {
-          const uint32_t scw = s_ < 4 ? sc03 : sc47, mw = s_ < 4 ? m03 : m47;
-          const int sh = 8 * (s_ & 3);
-          const float d1 = __fmul_rn(d, (float)((scw >> sh) & 0xFFu));   // ggml d1 = d * sc
-          const float m1 = __fmul_rn(dmin, (float)((mw >> sh) & 0xFFu));  // ggml m1 = dmin * m
-          const float c1 = __fmaf_rn(128.0f, d1, m1);                      // 128 d1 + m1 (exact 128 d1)
-          const uint32_t lo = qw[s_] & 0x0F0F0F0Fu, hi = (qw[s_] >> 4) & 0x0F0F0F0Fu;
-          typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-          // bytes [q, 0x43, q', 0x43] = bf16 (128 + q, 128 + q'): weights k .. k+7 in order
-          const u4v pk = {__builtin_amdgcn_perm(0x43434343u, lo, 0x04010400u),
-                          __builtin_amdgcn_perm(0x43434343u, lo, 0x04030402u),
-                          __builtin_amdgcn_perm(0x43434343u, hi, 0x04010400u),
-                          __builtin_amdgcn_perm(0x43434343u, hi, 0x04030402u)};
-          const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
-          const int ks = (sb0 + j) * 8 + s_;  // sub-block index in this block's K range
-          const int k = ks * 32 + 8 * g;
+        for (int m = 0; m < MT; ++m) {
+          const int xrow = min(m * 16 + fr, M - 1);
+          const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
+                               : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
+          // X_s = the sub-block's sum of each row's x: one more MFMA against ones, shared by
+          // the NT weight tiles (no separate pass over X, no barrier)
+          const f32x4 xs = mfma16(xf, ones, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-          for (int m = 0; m < MT; ++m) {
-            const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
-                                 : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
-            const f32x4 A = mfma16(xf, wf, f32x4{0.f, 0.f, 0.f, 0.f});
-            const f32x4 xs = *(const f32x4*)(xsum + ks * 16 * MT + m * 16 + 4 * g);
+          for (int n = 0; n < NT; ++n) {
+            // get_scale_min_k4 of sub-block s_ from the 12 scale bytes (header words y, z, w)
+            const uint4 h = hq[j][n];
+            const uint32_t scw = s_ < 4 ? (h.y & 0x3F3F3F3Fu) : ((h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u));
+            const uint32_t mw = s_ < 4 ? (h.z & 0x3F3F3F3Fu) : (((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u));
+            const float d1 = __fmul_rn(h2f(h.x), (float)((scw >> sh) & 0xFFu));        // ggml d1 = d * sc
+            const float m1 = __fmul_rn(h2f(h.x >> 16), (float)((mw >> sh) & 0xFFu));   // ggml m1 = dmin * m
+            const float c1 = __fmaf_rn(128.0f, d1, m1);                          // 128 d1 + m1 (exact 128 d1)
+            const uint4 qq = s_ < 4 ? q0[j][n] : q1[j][n];
+            const int si = s_ & 3;
+            const uint32_t qw = si == 0 ? qq.x : si == 1 ? qq.y : si == 2 ? qq.z : qq.w;
+            const uint32_t lo = qw & 0x0F0F0F0Fu, hi = (qw >> 4) & 0x0F0F0F0Fu;
+            // bytes [q, 0x43, q', 0x43] = bf16 (128 + q, 128 + q'): weights k .. k+7 in order
+            const u4v pk = {__builtin_amdgcn_perm(0x43434343u, lo, 0x04010400u),
+                            __builtin_amdgcn_perm(0x43434343u, lo, 0x04030402u),
+                            __builtin_amdgcn_perm(0x43434343u, hi, 0x04010400u),
+                            __builtin_amdgcn_perm(0x43434343u, hi, 0x04030402u)};
+            const f32x4 A = mfma16(xf, __builtin_bit_cast(bf16x8, pk), f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
             for (int i = 0; i < 4; ++i) acc[m][n][i] = __fmaf_rn(-c1, xs[i], __fmaf_rn(d1, A[i], acc[m][n][i]));
           }
@@ -369,12 +350,12 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
 static constexpr size_t kLdsCap = 160 * 1024;
 
 static bool qx_in_lds(int M, int K) {
-  return gemv_x_lds_bytes(M, K) + (size_t)(K / 32) * 16 * ((M + 15) / 16) * 4 <= kLdsCap;
+  return gemv_x_lds_bytes(M, K) <= kLdsCap;
 }
 
 static size_t qlds(const QPlan& p, int M, int K) {
-  // X image (when it fits) + the Q4_K sub-block sums [K/32][16*MT] fp32
-  const size_t xs = (qx_in_lds(M, K) ? gemv_x_lds_bytes(M, K) : 0) + (size_t)(K / 32) * 16 * p.MT * 4;
+  // X image (when it fits)
+  const size_t xs = qx_in_lds(M, K) ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
