@@ -54,6 +54,29 @@ __device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict_
   }
 }
 
+// where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip)
+enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
+constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave may hold (<= 32 VGPRs)
+// X source per GEMV family, measured same-box on MI355X at B = 8 (profiles/r02/v14_x_regs_ab.txt):
+// the K-quant GEMVs take X into registers (Q4_K_M decode 2.023 -> 1.950 ms/step: the dequant
+// work of each wave starts as soon as its own bytes land, with no block barrier), the bf16
+// GEMVs keep the LDS image (registers measured 2.25 -> 2.39 ms/step).  MS_GEMV_X=regs /
+// MS_QGEMV_X=lds flip them (A/B tuning).
+inline bool gemv_x_regs() {
+  static const bool v = [] {
+    const char* e = getenv("MS_GEMV_X");
+    return e && e[0] == 'r';
+  }();
+  return v;
+}
+inline bool qgemv_x_regs() {
+  static const bool v = [] {
+    const char* e = getenv("MS_QGEMV_X");
+    return !(e && e[0] == 'l');
+  }();
+  return v;
+}
+
 __device__ __forceinline__ void amax_merge_dev(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
 }

@@ -66,7 +66,13 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
 // Split-K (gridDim.y = S > 1, STORE_F32 only): block (x, y) covers k in [y*K, (y+1)*K) of
 // rows of length ldk and writes its fp32 partial to slab y = out + y*M*ldo; the consumer
 // (residual_rmsnorm_kernel) adds the S slabs in slab order -- deterministic, no atomics.
-template <int MT, int NT, int EPI, int U, bool XL>
+// XM = where the MFMA's X fragments come from:
+//   kXGlobal: global loads inside the MFMA loop (large M*K: no room in LDS or registers);
+//   kXLds:    the block's LDS image, copied by DMA ahead of the weight stream (gemv_dma_x);
+//   kXRegs:   each wave loads its OWN k-slice of X (the only part it multiplies) straight
+//             into registers ahead of its weight loads -- no LDS image, no block barrier,
+//             every wave starts its MFMAs as soon as its own bytes have landed.
+template <int MT, int NT, int EPI, int U, int XM>
 __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
@@ -82,8 +88,20 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
   }
 
-  // 1. X rows by LDS DMA first, then this wave's whole W stream (gemv_dma_x)
-  if constexpr (XL) gemv_dma_x(smem, X, M, K, ldk);
+  // 1. X first (LDS DMA of the block's rows, or this wave's slice into registers), then
+  // this wave's whole W stream: vmcnt retires in issue order
+  if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
+  uint4 xr[XM == kXRegs ? U : 1][XM == kXRegs ? MT : 1][2];
+  if constexpr (XM == kXRegs) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        const bf16_t* xg = X + (size_t)min(m * 16 + fr, M - 1) * ldk + kbeg + u * 64 + 16 * fg;
+        xr[u][m][0] = ldg16(xg);
+        xr[u][m][1] = ldg16(xg + 8);
+      }
+  }
   __builtin_amdgcn_sched_barrier(0);
   uint4 w[U][NT][2];
 #pragma unroll
@@ -95,9 +113,8 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       w[u][n][1] = ldw16(wp + u * 64 + 8);
     }
   }
-  // 2. the X image has landed once at most the W loads are pending -- or X fragments are
-  // read from L2 (large M*K)
-  if constexpr (XL) {
+  // 2. the X image has landed once at most the W loads are pending
+  if constexpr (XM == kXLds) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
     __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the W loads too
@@ -114,7 +131,10 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     for (int m = 0; m < MT; ++m) {
       const int xrow = min(m * 16 + fr, M - 1);
       bf16x8 x0, x1;
-      if constexpr (XL) {
+      if constexpr (XM == kXRegs) {
+        x0 = as_bf16x8(xr[u][m][0]);
+        x1 = as_bf16x8(xr[u][m][1]);
+      } else if constexpr (XM == kXLds) {
         const int k0 = kbeg + u * 64 + 16 * fg;
         x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
         x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
@@ -135,26 +155,33 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 
 template <int MT, int NT, int EPI, int U>
 static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
-                    int S, int ldo, const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+                    int S, int ldo, const GemvPlan& p, size_t lds, int xm, const GemvArgs& ga,
                     hipStream_t s) {
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
-    if (xl)
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, true>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+    if constexpr (MT * U <= kXRegsMaxFrags) {
+      if (xm == kXRegs) {
+        MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXRegs>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+                  ldo, ga);
+        return;
+      }
+    }
+    if (xm == kXLds)
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXLds>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
                 ldo, ga);
     else
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, false>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXGlobal>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
                 ldo, ga);
   }
 }
 
 template <int MT, int NT, int EPI>
 static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
-                      int S, int ldo, const GemvPlan& p, size_t lds, bool xl, const GemvArgs& ga,
+                      int S, int ldo, const GemvPlan& p, size_t lds, int xm, const GemvArgs& ga,
                       hipStream_t s) {
-#define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xl, ga, s)
+#define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xm, ga, s)
   switch (p.U) {
     case 1: GU(1); break;
     case 2: GU(2); break;
@@ -170,9 +197,9 @@ static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N,
 
 template <int MT>
 static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
-                       int S, int ldo, int epi, const GemvPlan& p, size_t lds, bool xl,
+                       int S, int ldo, int epi, const GemvPlan& p, size_t lds, int xm,
                        const GemvArgs& ga, hipStream_t s) {
-#define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xl, ga, s)
+#define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xm, ga, s)
   switch (epi) {
     case MS_GEMV_EPI_STORE_BF16: GE(1, MS_GEMV_EPI_STORE_BF16); break;
     case MS_GEMV_EPI_ADD_F32: GE(1, MS_GEMV_EPI_ADD_F32); break;
@@ -201,15 +228,17 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   const GemvPlan p = gemv_plan(M, N, K, epi, force_waves);
   if (p.waves == 0) return;  // callers check gemv_supported()
   const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
-  const size_t lds = gemv_lds_bytes(p, M, K, xl);
+  int xm = xl ? kXLds : kXGlobal;
+  if (gemv_x_regs() && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
+  const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds);
   if (lds > kMaxLds) return;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
   switch (p.MT) {
-    case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
-    case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
-    case 3: gemv_go_mt<3>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
-    default: gemv_go_mt<4>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xl, ga, s); break;
+    case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
+    case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
+    case 3: gemv_go_mt<3>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
+    default: gemv_go_mt<4>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
   }
 }
 

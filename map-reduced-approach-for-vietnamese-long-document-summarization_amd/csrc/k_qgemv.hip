@@ -183,7 +183,8 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 //         weights h*128 + {0,32,64,96} + l.
 // MFMA t of a super-block takes 8 of those weights per lane and the X elements of the
 // same k -- a k permutation applied to both operands, so every dot product is unchanged.
-template <int MT, int NT, int EPI, int SBW, bool XL>
+// XM: the X source (gemv_common.h kXGlobal / kXLds / kXRegs, as in k_gemv.hip)
+template <int MT, int NT, int EPI, int SBW, int XM>
 __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, GemvArgs ga) {
@@ -211,8 +212,26 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
     for (int n = 0; n < NT; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // X rows by LDS DMA first (gemv_dma_x), then the weight stream
+  constexpr bool XL = XM == kXLds, XR = XM == kXRegs;
+  // X first (LDS DMA of the block's rows, or this wave's super-blocks into registers), then
+  // the weight stream: vmcnt retires in issue order
   if constexpr (XL) gemv_dma_x(smem, X, M, K, ldx);
+  // Q4_K sub-block s of super-block j: lane group g's 8 weights at k = (j*8 + s)*32 + 8g;
+  // Q6_K MFMA t: k = j*256 + hh*128 + (t>>1)*32 + 16p + 8(t&1)
+  bf16x8 xr[XR ? SBW : 1][XR ? 8 : 1][XR ? MT : 1];
+  if constexpr (XR) {
+    const bool q6 = type != MS_QT_Q4_K;
+#pragma unroll
+    for (int j = 0; j < SBW; ++j)
+#pragma unroll
+      for (int t = 0; t < 8; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+          const int k = q6 ? (sb0 + j) * 256 + (g >> 1) * 128 + (t >> 1) * 32 + 16 * (g & 1) + 8 * (t & 1)
+                           : ((sb0 + j) * 8 + t) * 32 + 8 * g;
+          xr[j][t][m] = as_bf16x8(ldg16(X + (size_t)min(m * 16 + fr, M - 1) * ldx + k));
+        }
+  }
   __builtin_amdgcn_sched_barrier(0);
   if (type == MS_QT_Q4_K) {
     uint4 hq[SBW][NT], q0[SBW][NT], q1[SBW][NT];
@@ -241,7 +260,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int xrow = min(m * 16 + fr, M - 1);
-          const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
+          const bf16x8 xf = XR ? xr[XR ? j : 0][XR ? s_ : 0][XR ? m : 0]
+                          : XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
                                : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
           // X_s = the sub-block's sum of each row's x: one more MFMA against ones, shared by
           // the NT weight tiles (no separate pass over X, no barrier)
@@ -319,7 +339,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
+            const bf16x8 xf = XR ? xr[XR ? j : 0][XR ? t : 0][XR ? m : 0]
+                            : XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
                                  : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
@@ -353,9 +374,11 @@ static bool qx_in_lds(int M, int K) {
   return gemv_x_lds_bytes(M, K) <= kLdsCap;
 }
 
+static bool qx_in_regs(const QPlan& p) { return qgemv_x_regs() && p.MT * p.SBW == 1; }
+
 static size_t qlds(const QPlan& p, int M, int K) {
-  // X image (when it fits)
-  const size_t xs = qx_in_lds(M, K) ? gemv_x_lds_bytes(M, K) : 0;
+  // X image (when it fits and X is not taken into registers)
+  const size_t xs = (!qx_in_regs(p) && qx_in_lds(M, K)) ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
@@ -376,16 +399,17 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
     return;
   } else {
     const bool xl = qx_in_lds(M, K);
-#define QL(SBW_, XL_) \
-    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XL_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
-    if (p.SBW == 4 && xl) QL(4, true);
-    else if (p.SBW == 4) QL(4, false);
-    else if (p.SBW == 3 && xl) QL(3, true);
-    else if (p.SBW == 3) QL(3, false);
-    else if (p.SBW == 2 && xl) QL(2, true);
-    else if (p.SBW == 2) QL(2, false);
-    else if (xl) QL(1, true);
-    else QL(1, false);
+#define QL(SBW_, XM_) \
+    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
+    if (p.SBW == 4 && xl) QL(4, kXLds);
+    else if (p.SBW == 4) QL(4, kXGlobal);
+    else if (p.SBW == 3 && xl) QL(3, kXLds);
+    else if (p.SBW == 3) QL(3, kXGlobal);
+    else if (p.SBW == 2 && xl) QL(2, kXLds);
+    else if (p.SBW == 2) QL(2, kXGlobal);
+    else if (xl && !qx_in_regs(p)) QL(1, kXLds);
+    else if (!qx_in_regs(p)) QL(1, kXGlobal);
+    else if constexpr (MT == 1) QL(1, kXRegs);
 #undef QL
   }
 }
