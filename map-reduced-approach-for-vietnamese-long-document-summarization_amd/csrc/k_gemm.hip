@@ -108,6 +108,34 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
   }
 
   // epilogue: acc[m][n][j] = C[row 4*fg + j][col fr] of 16x16 tile (m, n)
+  if constexpr (EPI == 1) {  // residual add: 32 loads in flight, then the adds and stores
+#pragma unroll
+    for (int m0_ = 0; m0_ < 4; m0_ += 2) {
+      float r[2][4][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const int row = min(m0 + wm * 64 + (m0_ + h) * 16 + fg * 4 + j, M - 1);
+            const int col = min(n0 + wn * 64 + n * 16 + fr, N - 1);
+            r[h][j][n] = __builtin_nontemporal_load(((const float*)out) + (size_t)row * ldo + col);
+          }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int n = 0; n < 4; ++n) {
+            const int row = m0 + wm * 64 + (m0_ + h) * 16 + fg * 4 + j;
+            const int col = n0 + wn * 64 + n * 16 + fr;
+            if (row < M && col < N) ((float*)out)[(size_t)row * ldo + col] = r[h][j][n] + acc[m0_ + h][n][j];
+          }
+    }
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
 #pragma unroll
@@ -298,6 +326,40 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 
   // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x64
+  if constexpr (EPI == 1) {
+    // residual add: the 32 fp32 loads of two 16-row groups are issued together before their
+    // adds and stores (a plain `out[o] += acc` compiled to 128 dependent load -> wait ->
+    // store round trips per lane)
+#pragma unroll
+    for (int mi0 = 0; mi0 < 8; mi0 += 2) {
+      float r[2][4][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            // clamped rows/cols: every load is in bounds and unconditional (one basic block)
+            const int row = min(m0 + wr * 128 + (mi0 + h) * 16 + fg * 4 + j, M - 1);
+            const int col = min(n0 + wc * 64 + ni * 16 + fr, N - 1);
+            r[h][j][ni] = __builtin_nontemporal_load(((const float*)out) + (size_t)row * ldo + col);
+          }
+      // keep the batch: under 216 live VGPRs the scheduler would otherwise sink every load
+      // next to its store (one round trip per element)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) {
+            const int row = m0 + wr * 128 + (mi0 + h) * 16 + fg * 4 + j;
+            const int col = n0 + wc * 64 + ni * 16 + fr;
+            if (row < M && col < N) ((float*)out)[(size_t)row * ldo + col] = r[h][j][ni] + acc[mi0 + h][ni][j];
+          }
+    }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
