@@ -1353,7 +1353,8 @@ int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int3
   return op_guard([&] {
     REQUIRE(X && packed && out && N >= 16, MS_EINVAL, "bad qgemv operands");
     REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
-    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0),
+            MS_EINVAL, "bad epilogue");
     REQUIRE(qgemv_supported(M, N, K, epi), MS_EINVAL, "qgemv shape unsupported (M<=64, K%256==0, N%16==0)");
     QMat q{};
     q.n = 1;

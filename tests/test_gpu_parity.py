@@ -575,6 +575,31 @@ def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
 
 
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
+@pytest.mark.parametrize("M", [1, 8, 33])
+@pytest.mark.parametrize("N,K", [(4096, 768), (1040, 3072)])
+def test_qgemv_argmax_vs_fp64(lib, dev, qtype, M, N, K):
+    """The quantised lm_head epilogue (config 5's Q6_K vocab matrix): {max, id} partials per
+    16-column tile merge to the fp64 argmax of the dequantised product, unless the top two
+    are within fp32 noise."""
+    b, wbf, pk = _packed(lib, dev, qtype, N, K, 5 + M)
+    g = torch.Generator(device="cpu").manual_seed(3 * M + N + K)
+    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    ref = X.double().cpu() @ _decode_weights(qtype, b, wbf).T
+    part = torch.full((M, N // 16, 2), float("nan"), device=dev)
+    ids = torch.empty(M, dtype=torch.int32, device=dev)
+    L.check(lib.ms_op_qgemv(X.data_ptr(), qtype, pk.data_ptr(), part.data_ptr(), M, N, K, N // 16,
+                            L.MS_EPI_ARGMAX, _stream()))
+    L.check(lib.ms_op_argmax_partials(part.data_ptr(), M, N // 16, ids.data_ptr(), _stream()))
+    torch.cuda.synchronize()
+    assert not torch.isnan(part).any(), "every 16-column tile writes its partial"
+    srt = torch.sort(ref, 1).values
+    got = ids.cpu().long()
+    for r in range(M):
+        if srt[r, -1] - srt[r, -2] > 1e-4 * (abs(float(srt[r, -1])) + 1.0):
+            assert int(got[r]) == int(torch.argmax(ref[r])), r
+
+
+@pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("N,K,S", [(256, 3072, 6), (512, 3072, 4), (128, 8192, 4), (256, 8192, 2),
                                    (64, 768, 3)])
