@@ -348,27 +348,36 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   bf16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
   bf16_t* vn = kn + kHeadDim;                 // [128] v of the new token
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
+  constexpr int NWB = kSplitPages;  // waves per block: a wave's pages are NWB apart
 
-  // K fragments (16 rows x 64 B per instruction) and V rows (1 KB) of one page
+  // K fragments (16 rows x 64 B per instruction) and V rows (1 KB) of one page, by physical
+  // page id
   u32x4 kf[4][4], vr[16];
-  auto fetch_k = [&](int pg) {
-    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  auto fetch_k = [&](int pid) {
+    const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
         kf[mt][s4] = ld_stream(kv.k + base + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
   };
-  auto fetch_v = [&](int pg) {
-    const size_t base = ((size_t)bt[pg] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  auto fetch_v = [&](int pid) {
+    const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 #pragma unroll
     for (int i = 0; i < 16; ++i)
       vr[i] = ld_stream(kv.v + base + (i * 4 + (lane >> 4)) * kHeadDim + (lane & 15) * 8);
   };
+  // the block-table entries of the unrolled plan's two pages load together, before any
+  // page: the second page's prefetch (issued under the first page's math) then needs no
+  // table round trip of its own (vmcnt retires in order: a table load issued there would
+  // also wait for everything before it)
+  int pid_next = 0;
+  if constexpr (PPWT == 2) pid_next = pg0 + NWB < pend ? bt[pg0 + NWB] : 0;
   // issue the first page first, so its HBM latency overlaps the q/k/v prologue
   if (pg0 < pend) {
-    fetch_k(pg0);
-    fetch_v(pg0);
+    const int pid0 = bt[pg0];
+    fetch_k(pid0);
+    fetch_v(pid0);
   }
 
   if constexpr (FROM_SLABS) {
@@ -463,7 +472,8 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
       }
-      if (more) fetch_k(pg + kSplitPages);  // K registers are free: next page's K in flight
+      const int pid_n = PPWT == 2 ? pid_next : (more ? bt[pg + kSplitPages] : 0);
+      if (more) fetch_k(pid_n);  // K registers are free: next page's K in flight
       float mx = -INFINITY;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -501,7 +511,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
         if (patch && row == off) vr[i] = *(const u32x4*)(vn + (lane & 15) * 8);
         *(u32x4*)(vs_ + v_swz(row, lane & 15)) = vr[i];
       }
-      if (more) fetch_v(pg + kSplitPages);  // V registers are free: next page's V in flight
+      if (more) fetch_v(pid_n);  // V registers are free: next page's V in flight
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the V image is in LDS
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -599,12 +609,17 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
                                                                   bf16_t* __restrict__ out, int Hq,
                                                                   int nsplit) {
-  // every (m_s, l_s) pair is loaded at once (wave 0, two splits per lane) and the O loads
-  // are issued 8 at a time: the old serial split loop was a chain of dependent L2 round
-  // trips.  Sums keep the split order, so results are unchanged.
+  // one memory round trip: every (m_s, l_s) pair (wave 0, two splits per lane) and, for
+  // nsplit <= 16, every O value of this thread are loaded before the barrier (the O loads
+  // do not depend on the split weights); sums keep the split order, so results are unchanged
   __shared__ float fw[128], lw[128];
   const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
   const float* p = ws + ((size_t)b * Hq + hq) * nsplit * 132;
+  const float* po = p + 2 + d;
+  constexpr int kPre = 16;
+  float ov[kPre];
+#pragma unroll
+  for (int q = 0; q < kPre; ++q) ov[q] = po[min(q, nsplit - 1) * 132];
   if (d < 64) {
     const float m0 = d < nsplit ? p[d * 132] : -INFINITY;
     const float m1 = d + 64 < nsplit ? p[(d + 64) * 132] : -INFINITY;
@@ -620,19 +635,14 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
   }
   __syncthreads();
   float L = 0.f, O = 0.f;
-  const float* po = p + 2 + d;
-  int s = 0;
-  for (; s + 8 <= nsplit; s += 8) {
-    float v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = po[(s + q) * 132];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      L += fw[s + q] * lw[s + q];
-      O += fw[s + q] * v[q];
+  for (int q = 0; q < kPre; ++q) {
+    if (q < nsplit) {
+      L += fw[q] * lw[q];
+      O += fw[q] * ov[q];
     }
   }
-  for (; s < nsplit; ++s) {
+  for (int s = kPre; s < nsplit; ++s) {
     L += fw[s] * lw[s];
     O += fw[s] * po[s * 132];
   }

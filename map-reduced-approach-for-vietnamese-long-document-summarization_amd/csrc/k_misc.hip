@@ -100,27 +100,37 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
   float* xr = x + (size_t)r * H;
   const int n4 = H / 4;
   const size_t slab = (size_t)rows * H;
-  float4 v[KMAX], p[KMAX][S > 0 ? S : 1];
-  uint2 wv[KMAX];
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  f32x4 v[KMAX], p[KMAX][S > 0 ? S : 1];
+  u32x2 wv[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     const int c = min((int)threadIdx.x + k * 256, n4 - 1);
-    v[k] = *(const float4*)(xr + c * 4);
-    wv[k] = *(const uint2*)(w + c * 4);
+    v[k] = *(const f32x4*)(xr + c * 4);
+    wv[k] = *(const u32x2*)(w + c * 4);
 #pragma unroll
-    for (int q = 0; q < S; ++q) p[k][q] = *(const float4*)(slabs + q * slab + (size_t)r * H + c * 4);
+    for (int q = 0; q < S; ++q) p[k][q] = *(const f32x4*)(slabs + q * slab + (size_t)r * H + c * 4);
+  }
+  // every load above is in flight before the first add (one memory round trip), and the
+  // residual stores wait until after the row reduction (on gfx9 stores count in vmcnt, so a
+  // store between the loads and their last use makes the reduction wait for it too).  The
+  // empty asm statements make every loaded value opaque here, so no add is hoisted between
+  // the loads (the compiler otherwise interleaves them and issues the loads in three waves).
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) {
+    asm volatile("" : "+v"(v[k]));
+    asm volatile("" : "+v"(wv[k]));
+#pragma unroll
+    for (int q = 0; q < S; ++q) asm volatile("" : "+v"(p[k][q]));
   }
   if constexpr (S > 0) {
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
-      float4 a = p[k][0];
+      f32x4 acc = p[k][0];
 #pragma unroll
-      for (int q = 1; q < S; ++q) {
-        a.x += p[k][q].x; a.y += p[k][q].y; a.z += p[k][q].z; a.w += p[k][q].w;
-      }
-      v[k].x += a.x; v[k].y += a.y; v[k].z += a.z; v[k].w += a.w;
-      const int c = threadIdx.x + k * 256;
-      if (c < n4) *(float4*)(xr + c * 4) = v[k];
+      for (int q = 1; q < S; ++q) acc += p[k][q];
+      v[k] += acc;
     }
   }
   float ss = 0.f;
@@ -137,6 +147,7 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
   for (int k = 0; k < KMAX; ++k) {
     const int c = threadIdx.x + k * 256;
     if (c >= n4) break;
+    if constexpr (S > 0) *(f32x4*)(xr + c * 4) = v[k];
     const float g0 = __uint_as_float(wv[k].x << 16), g1 = __uint_as_float(wv[k].x & 0xFFFF0000u);
     const float g2 = __uint_as_float(wv[k].y << 16), g3 = __uint_as_float(wv[k].y & 0xFFFF0000u);
     uint2 o;
