@@ -91,6 +91,7 @@ struct ms_engine {
   hipStream_t stream = nullptr;
   int H = 0, Hq = 0, Hk = 0, D = 128, F = 0, V = 0, L = 0, QKVN = 0;
   int max_pages = 0, n_pages = 0, Tmax = 0;
+  bool slot_major = false;  // pool of max_batch x max_pages: slot s owns pages [s*max_pages, +max_pages)
   std::vector<void*> allocs;
   std::vector<Layer> layers;
   std::vector<std::array<QSlot, 4>> lq;  // per layer: QKV, O, gate/up, down
@@ -197,6 +198,7 @@ struct ms_engine {
     v.block_table = bt_d;
     v.max_pages = max_pages;
     v.n_kv_heads = Hk;
+    v.slot_major = slot_major ? 1 : 0;
     return v;
   }
 
@@ -488,6 +490,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.QKVN = (E.Hq + 2 * E.Hk) * E.D;
     E.max_pages = (cfg->max_ctx + kPage - 1) / kPage;
     E.n_pages = cfg->n_pages > 0 ? cfg->n_pages : cfg->max_batch * E.max_pages;
+    E.slot_major = E.n_pages == cfg->max_batch * E.max_pages && !getenv("MS_KV_PAGED");
     E.Tmax = std::max(cfg->max_prefill_tokens, cfg->max_batch);
     // weights
     E.embed = E.dalloc<bf16_t>((size_t)E.V * E.H);
@@ -912,7 +915,8 @@ static void reserve(ms_engine& E, Seq& s, int tokens) {
   E.free_slots.pop_back();
   const int need = (tokens + kPage - 1) / kPage;
   for (int i = 0; i < need; ++i) {
-    s.pages.push_back(E.free_pages.back());
+    // slot-major pool: the free list only counts pages; the slot's own range is used
+    s.pages.push_back(E.slot_major ? s.slot * E.max_pages + i : E.free_pages.back());
     E.free_pages.pop_back();
   }
   int32_t* row = &E.bt_h[(size_t)s.slot * E.max_pages];

@@ -61,7 +61,8 @@ __device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
 __device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], const KVView& kv,
                                               const int32_t* bt, int kvh, int t, int kvlen,
                                               int tid) {
-  const size_t base = ((size_t)bt[t] * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];  // bt = the slot's row
+  const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
   const int row = tid >> 4, ch = tid & 15;
   kr[0] = *(const u32x4*)(kv.k + base + (row + 0) * kHeadDim + ch * 8);
   kr[1] = *(const u32x4*)(kv.k + base + (row + 16) * kHeadDim + ch * 8);
@@ -371,11 +372,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   // page: the second page's prefetch (issued under the first page's math) then needs no
   // table round trip of its own (vmcnt retires in order: a table load issued there would
   // also wait for everything before it)
+  // (a slot-major pool needs no table at all)
+  auto page_id = [&](int pg) { return kv.slot_major ? slot * kv.max_pages + pg : bt[pg]; };
   int pid_next = 0;
-  if constexpr (PPWT == 2) pid_next = pg0 + NWB < pend ? bt[pg0 + NWB] : 0;
+  if constexpr (PPWT == 2) pid_next = pg0 + NWB < pend ? page_id(pg0 + NWB) : 0;
   // issue the first page first, so its HBM latency overlaps the q/k/v prologue
   if (pg0 < pend) {
-    const int pid0 = bt[pg0];
+    const int pid0 = page_id(pg0);
     fetch_k(pid0);
     fetch_v(pid0);
   }
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     if (owns_new && tid < kHeadDim) vn[tid] = f2bf(raw[(G + 1) * kHeadDim + tid]);
     __syncthreads();  // raw consumed (wave 0 may stage V); qn/kn/vn ready
     if (owns_new && tid < kHeadDim) {  // the new token's K/V into the cache, for later steps
-      const int page = bt[pos / kPage];
+      const int page = page_id(pos / kPage);
       const size_t o = (((size_t)page * kv.n_kv_heads + kvh) * kPage + pos % kPage) * kHeadDim + tid;
       kv.k[o] = kn[tid];
       kv.v[o] = vn[tid];
@@ -472,7 +475,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
       }
-      const int pid_n = PPWT == 2 ? pid_next : (more ? bt[pg + kSplitPages] : 0);
+      const int pid_n = PPWT == 2 ? pid_next : (more ? page_id(pg + kSplitPages) : 0);
       if (more) fetch_k(pid_n);  // K registers are free: next page's K in flight
       float mx = -INFINITY;
 #pragma unroll

@@ -11,6 +11,9 @@ struct KVView {
   const int32_t* block_table;  // [slots][max_pages]
   int32_t max_pages;           // row stride of block_table
   int32_t n_kv_heads;
+  // 1: slot-major pool (the engine's default sizing, max_batch x max_pages pages): logical
+  // page p of slot s is page s*max_pages + p, so decode attention needs no table lookup
+  int32_t slot_major;
 };
 
 // Prefill attention work description (device arrays, see engine.cpp StepArgs).

@@ -431,6 +431,23 @@ def test_continuous_batching_more_chunks_than_slots(dev):
         e.close()
 
 
+@pytest.mark.parametrize("n_pages", [0, 20])
+def test_paged_pool_matches_slot_major(dev, n_pages):
+    """The default pool (max_batch x max_pages, slot-major: no block-table lookups in the
+    attention kernels) and an explicitly sized pool whose pages are recycled in arbitrary
+    order through the block table give the same tokens, with more chunks than slots."""
+    prompts = [_prompt(n, 900 + n) for n in (100, 250, 300, 7, 180, 90, 400)]
+    outs = []
+    for pages in (0, n_pages):
+        e = Engine(TINY, device=0, max_batch=3, max_ctx=512, max_prefill_tokens=600, n_pages=pages)
+        try:
+            e.init_synthetic(SEED, STD, JITTER)
+            outs.append([r.ids for r in e.generate(prompts, num_predict=10, ignore_eos=True)])
+        finally:
+            e.close()
+    assert outs[0] == outs[1]
+
+
 def test_errors_are_reported(dev):
     e = Engine(TINY, device=0, max_batch=2, max_ctx=128, max_prefill_tokens=128)
     try:
