@@ -47,7 +47,6 @@ __device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// one 64-key K/V tile (16 KB each) into registers, 4 x 16 B per thread, coalesced rows
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // decode KV pages are read once per step: non-temporal when MS_NT_STREAM is set
 __device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
@@ -56,27 +55,6 @@ __device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
 #else
   return *(const u32x4*)p;
 #endif
-}
-
-__device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], const KVView& kv,
-                                              const int32_t* bt, int kvh, int t, int kvlen,
-                                              int tid) {
-  const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];  // bt = the slot's row
-  const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
-  const int row = tid >> 4, ch = tid & 15;
-  kr[0] = *(const u32x4*)(kv.k + base + (row + 0) * kHeadDim + ch * 8);
-  kr[1] = *(const u32x4*)(kv.k + base + (row + 16) * kHeadDim + ch * 8);
-  kr[2] = *(const u32x4*)(kv.k + base + (row + 32) * kHeadDim + ch * 8);
-  kr[3] = *(const u32x4*)(kv.k + base + (row + 48) * kHeadDim + ch * 8);
-  vr[0] = *(const u32x4*)(kv.v + base + (row + 0) * kHeadDim + ch * 8);
-  vr[1] = *(const u32x4*)(kv.v + base + (row + 16) * kHeadDim + ch * 8);
-  vr[2] = *(const u32x4*)(kv.v + base + (row + 32) * kHeadDim + ch * 8);
-  vr[3] = *(const u32x4*)(kv.v + base + (row + 48) * kHeadDim + ch * 8);
-  const int lim = kvlen - t * 64;  // rows >= lim are past the sequence: never feed stale V to P.V
-  if (row + 0 >= lim) vr[0] = u32x4{0, 0, 0, 0};
-  if (row + 16 >= lim) vr[1] = u32x4{0, 0, 0, 0};
-  if (row + 32 >= lim) vr[2] = u32x4{0, 0, 0, 0};
-  if (row + 48 >= lim) vr[3] = u32x4{0, 0, 0, 0};
 }
 
 // ============================================================ prefill (varlen, causal)
@@ -88,14 +66,17 @@ __device__ __forceinline__ void fetch_kv_tile(u32x4 (&kr)[4], u32x4 (&vr)[4], co
 // on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)); the O rescale is skipped when no
 // query column of the wave raised its max (alpha == 1 exactly); the causal / sequence-end
 // mask is applied only on tiles that can cross it.
+// K/V tiles reach LDS by DMA (global_load_lds, no register staging and no ds_write), two
+// buffers: tile t+1 is in flight while tile t is multiplied, one barrier per tile.  The
+// swizzles are applied on the DMA source (lane i of a 1-KiB piece lands at chunk i % 16 of
+// row i / 16, so it loads the global chunk that belongs there); rows past the sequence
+// load the last valid row instead (finite values under P = 0: never NaN * 0 in P.V).
 template <int GB>
 __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __restrict__ qkv,
                                                               bf16_t* __restrict__ out, int Hq,
                                                               int Hk, KVView kv, PrefillAttnArgs a,
                                                               float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[32768];
-  char* ks_ = smem;
-  char* vs_ = smem + 16384;
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int ngrp = Hq / GB;
@@ -133,23 +114,33 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
   const int ntiles = (kv_end + 63) / 64;
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
 
-  u32x4 kreg[4], vreg[4];
-  fetch_kv_tile(kreg, vreg, kv, bt, kvh, 0, kvlen, tid);
-  for (int t = 0; t < ntiles; ++t) {
-    __syncthreads();  // previous tile fully consumed
-    {
-      const int row = tid >> 4, ch = tid & 15;
-      *(u32x4*)(ks_ + k_swz(row, ch)) = kreg[0];
-      *(u32x4*)(ks_ + k_swz(row + 16, ch)) = kreg[1];
-      *(u32x4*)(ks_ + k_swz(row + 32, ch)) = kreg[2];
-      *(u32x4*)(ks_ + k_swz(row + 48, ch)) = kreg[3];
-      *(u32x4*)(vs_ + v_swz(row, ch)) = vreg[0];
-      *(u32x4*)(vs_ + v_swz(row + 16, ch)) = vreg[1];
-      *(u32x4*)(vs_ + v_swz(row + 32, ch)) = vreg[2];
-      *(u32x4*)(vs_ + v_swz(row + 48, ch)) = vreg[3];
+  // this wave's 8 DMA pieces of a tile: piece J = 8*wave + i covers rows 4(J % 16) ..+3 of
+  // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
+  auto dma_tile = [&](int t, int buf) {
+    const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];
+    const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+    const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
+    char* img = smem + buf * 32768;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int J = 8 * wave + i, isv = J >> 4;
+      const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
+      const int srow = min(row, lim - 1);
+      const int sch = isv ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
+      const bf16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (LDS_AS void*)(img + isv * 16384 + 4 * (J & 15) * 256), 16, 0, 0);
     }
-    __syncthreads();
-    if (t + 1 < ntiles) fetch_kv_tile(kreg, vreg, kv, bt, kvh, t + 1, kvlen, tid);  // next tile's HBM reads overlap this tile's math
+  };
+  dma_tile(0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t landed (its DMA is the only global load in flight), and every wave is past
+    // tile t-1, whose buffer the next DMA overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < ntiles) dma_tile(t + 1, (t + 1) & 1);
+    const char* ks_ = smem + (t & 1) * 32768;
+    const char* vs_ = ks_ + 16384;
 
     f32x4 sc[GB][4];
 #pragma unroll
