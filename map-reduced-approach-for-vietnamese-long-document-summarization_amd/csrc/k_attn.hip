@@ -35,9 +35,9 @@ __device__ __forceinline__ bf16x8 load_vt(const char* vs, int dt, int ks, int la
   typedef short s4 __attribute__((ext_vector_type(4)));
   s4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4*)(vs + v_swz(r0, ch) + sub));
   s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4*)(vs + v_swz(r1, ch) + sub));
-  typedef short s8 __attribute__((ext_vector_type(8)));
-  s8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
-  return __builtin_bit_cast(bf16x8, c);
+  // a vector concatenation (register adjacency): building the 8 shorts element by element
+  // compiled to sdwa or/shift repacking, ~80 VALU instructions per attention tile
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
 // B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1
@@ -63,9 +63,9 @@ __device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
 // Each K fragment read from LDS feeds GB MFMAs (S^T of the GB heads) and each V^T fragment
 // GB MFMAs (O^T of the GB heads): LDS read traffic per MFMA drops GB-fold, and a K/V tile
 // is fetched from HBM once per GB heads instead of once per head.  The online softmax works
-// on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)); the O rescale is skipped when no
-// query column of the wave raised its max (alpha == 1 exactly); the causal / sequence-end
-// mask is applied only on tiles that can cross it.
+// on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)) with a lazily moved reference
+// max (below); the O rescale is skipped when no query column of the wave moved it; the
+// causal / sequence-end mask is applied only on tiles that can cross it.
 // K/V tiles reach LDS by DMA (global_load_lds, no register staging and no ds_write), two
 // buffers: tile t+1 is in flight while tile t is multiplied, one barrier per tile.  The
 // swizzles are applied on the DMA source (lane i of a 1-KiB piece lands at chunk i % 16 of
@@ -76,7 +76,8 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
                                                               bf16_t* __restrict__ out, int Hq,
                                                               int Hk, KVView kv, PrefillAttnArgs a,
                                                               float scale_log2) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768];
+  // [K|V tile buffer 0][K|V tile buffer 1][Q of the GB heads, 16 KB each]
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + GB * 16384];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int ngrp = Hq / GB;
@@ -91,13 +92,18 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
   const int qpos = kvlen - qlen + qi;
   const int wave_qpos0 = kvlen - qlen + qb * 64 + wave * 16;  // the wave's first query
 
-  bf16x8 qf[GB][4];
+  // Q fragments live in LDS (each wave reads back only its own 16 rows, swizzled like K):
+  // held in registers they pushed the GB = 3 kernel past 256 VGPRs, and the compiler then
+  // shuttled values through AGPRs (~700 v_accvgpr moves)
+  char* qimg = smem + 2 * 32768;
+  const int qrow_l = wave * 16 + r;
   {
     const bf16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h0 * kHeadDim;
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) qf[hh][s] = as_bf16x8(*(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g));
+      for (int s = 0; s < 4; ++s)
+        *(uint4*)(qimg + hh * 16384 + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
   }
   f32x4 o[GB][8];
   float m_run[GB], l_run[GB];
@@ -151,7 +157,8 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       for (int s = 0; s < 4; ++s) {
         const bf16x8 kf = *(const bf16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
 #pragma unroll
-        for (int hh = 0; hh < GB; ++hh) sc[hh][mt] = mfma16(kf, qf[hh][s], sc[hh][mt]);
+        for (int hh = 0; hh < GB; ++hh)
+          sc[hh][mt] = mfma16(kf, *(const bf16x8*)(qimg + hh * 16384 + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
       }
     }
     // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
@@ -180,10 +187,16 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
         for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sc[hh][mt][j]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      // lazy rescale: the running max only moves when a tile's max exceeds it by more than
+      // 8 in log2 units (p <= 2^8 is harmless in fp32 and for the bf16 rounding of P), so
+      // after the first tiles the O accumulators (held in AGPRs) are rarely rescaled;
+      // O / l is unchanged by the choice of reference max
       const float m_new = fmaxf(m_run[hh], mx);
-      alpha[hh] = (m_run[hh] == m_new) ? 1.f : __builtin_amdgcn_exp2f((m_run[hh] - m_new) * scale_log2);
-      rescale |= (m_run[hh] != m_new);
-      const float mc = (m_new == -INFINITY) ? 0.f : m_new * scale_log2;
+      const bool grow = m_new != m_run[hh] && !((m_new - m_run[hh]) * scale_log2 <= 8.f);
+      const float m_use = grow ? m_new : m_run[hh];
+      alpha[hh] = grow ? __builtin_amdgcn_exp2f((m_run[hh] - m_new) * scale_log2) : 1.f;
+      rescale |= grow;
+      const float mc = (m_use == -INFINITY) ? 0.f : m_use * scale_log2;
       float rs = 0.f;
 #pragma unroll
       for (int mt = 0; mt < 4; ++mt)
@@ -196,7 +209,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       rs += __shfl_xor(rs, 16, 64);
       rs += __shfl_xor(rs, 32, 64);
       l_run[hh] = l_run[hh] * alpha[hh] + rs;
-      m_run[hh] = m_new;
+      m_run[hh] = m_use;
       pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
     }
