@@ -143,7 +143,9 @@ struct ms_engine {
   // kernels' pointers and the step-argument layout depend on nothing else
   std::map<std::pair<int, int>, hipGraphExec_t> decode_graphs;
   bool use_graphs = true;
-  int32_t* ids_host = nullptr;  // pinned landing buffer for the next greedy ids
+  int32_t* ids_host = nullptr;  // pinned ring: kMaxRun steps x max_batch greedy ids
+  static constexpr int kMaxRun = 64;  // chained decode steps per host synchronisation
+  int max_run = kMaxRun;              // MS_DECODE_RUN (1 = one step per ms_step)
 
   template <class T>
   T* dalloc(size_t n, bool zero = false) {
@@ -551,7 +553,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
-    HIP_OK(hipHostMalloc((void**)&E.ids_host, cfg->max_batch * sizeof(int32_t), hipHostMallocDefault));
+    HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * std::max(cfg->max_batch, 256) * sizeof(int32_t),
+                         hipHostMallocDefault));
+    if (const char* v = getenv("MS_DECODE_RUN")) E.max_run = std::max(1, std::min(atoi(v), (int)ms_engine::kMaxRun));
     if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
     HIP_OK(hipDeviceSynchronize());
     return MS_OK;
@@ -1041,10 +1045,19 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
     E.prof_end(K_MISC);
   }
+  // the next chained step's arguments, on the device (decode_run)
+  launch_decode_advance(d, E.ids_out_d, B, E.V, E.stream);
 }
 
-// one greedy decode step for every running sequence (B rows of one token each)
-static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int32_t>& next) {
+// k chained greedy decode steps for every sequence of `batch` (B rows of one token each)
+// with ONE host synchronisation: the arguments are uploaded once, each step's argmax ids
+// feed the next step on the device (decode_advance), and each step's ids are copied to a
+// pinned ring.  The caller picks k so that no sequence reaches num_predict inside the run
+// and the split grid of decode attention (longest sequence rounded up to 256 keys) does not
+// change; a sequence that stops early (EOS, failed row) keeps computing until the run ends
+// and its extra tokens are dropped -- its reserved pages hold them, and no other row
+// depends on it (batch-invariant kernels).  ids[j * B + i] = token of row i at step j.
+static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vector<int32_t>& ids) {
   const int B = (int)batch.size();
   std::vector<int32_t> a;
   a.reserve(4 * B);
@@ -1060,8 +1073,9 @@ static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int3
   da.seq_slot = d + 2 * (size_t)B;
   da.B = B;
   // the split grid only depends on the longest sequence rounded up to 256 keys
-  da.max_len = ((max_len + 255) / 256) * 256;
+  da.max_len = ((max_len + k - 1 + 255) / 256) * 256;
   da.ppw = E.attn_ppw;
+  hipGraphExec_t ex = nullptr;
   if (E.use_graphs && E.prof_mask == 0) {
     const auto key = std::make_pair(B, da.max_len);
     auto it = E.decode_graphs.find(key);
@@ -1070,21 +1084,23 @@ static void decode_step(ms_engine& E, std::vector<Seq*>& batch, std::vector<int3
       HIP_OK(hipStreamBeginCapture(E.stream, hipStreamCaptureModeRelaxed));
       decode_body(E, B, d, da);
       HIP_OK(hipStreamEndCapture(E.stream, &g));
-      hipGraphExec_t ex = nullptr;
       HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       HIP_OK(hipGraphDestroy(g));
       it = E.decode_graphs.emplace(key, ex).first;
     }
-    HIP_OK(hipGraphLaunch(it->second, E.stream));
-  } else {
-    decode_body(E, B, d, da);
+    ex = it->second;
   }
-  HIP_OK(hipGetLastError());
+  for (int j = 0; j < k; ++j) {
+    if (ex) HIP_OK(hipGraphLaunch(ex, E.stream));
+    else decode_body(E, B, d, da);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(E.ids_host + (size_t)j * B, E.ids_out_d, B * sizeof(int32_t),
+                          hipMemcpyDeviceToHost, E.stream));
+  }
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
-  HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_out_d, B * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
-  next.resize(B);
+  ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
-  std::memcpy(next.data(), E.ids_host, B * sizeof(int32_t));
+  std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));
 }
 
 int ms_step(ms_engine* e) {
@@ -1125,25 +1141,37 @@ int ms_step(ms_engine* e) {
         accept_token(E, s, first[i]);
       }
     }
-    // 3. one decode step for every running sequence that still needs tokens
+    // 3. decode every running sequence that still needs tokens: a run of k chained steps
+    // (one host synchronisation), k bounded by the nearest num_predict, the attention split
+    // grid and kMaxRun; k = 1 while admissible work waits for a free slot
     std::vector<Seq*> batch;
     for (auto& s : E.running)
       if (!s->finish) batch.push_back(s.get());
     for (size_t i0 = 0; i0 < batch.size(); i0 += 256) {
       std::vector<Seq*> sub(batch.begin() + i0, batch.begin() + std::min(batch.size(), i0 + 256));
-      std::vector<int32_t> next;
-      decode_step(E, sub, next);  // records ev_a/ev_b around its device work and syncs
+      int k = (batch.size() > 256 || (!E.waiting.empty() && !E.free_slots.empty())) ? 1 : E.max_run;
+      int max_len = 0;
+      for (Seq* s : sub) {
+        k = std::min(k, s->num_predict - (int)s->out.size());
+        max_len = std::max(max_len, s->len + 1);
+      }
+      k = std::max(1, std::min(k, ((max_len + 255) / 256) * 256 - max_len + 1));
+      std::vector<int32_t> ids;
+      decode_run(E, sub, k, ids);  // records ev_a/ev_b around its device work and syncs
       float ms_ = 0.f;
       HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
       E.stats.decode_ms += ms_;
       E.prof_collect();
-      E.stats.decode_steps += 1;
-      E.stats.decode_tokens += (int64_t)sub.size();
-      for (size_t i = 0; i < sub.size(); ++i) {
-        E.stats.decode_kv_tokens += sub[i]->len + 1;
-        sub[i]->len += 1;
-        accept_token(E, *sub[i], next[i]);
-      }
+      E.stats.decode_steps += k;
+      E.stats.decode_tokens += (int64_t)sub.size() * k;
+      for (int j = 0; j < k; ++j)
+        for (size_t i = 0; i < sub.size(); ++i) {
+          Seq& s = *sub[i];
+          if (s.finish) continue;  // stopped earlier in the run: drop the rest
+          E.stats.decode_kv_tokens += s.len + 1;
+          s.len += 1;
+          accept_token(E, s, ids[(size_t)j * sub.size() + i]);
+        }
     }
     // 4. retire finished sequences
     for (auto it = E.running.begin(); it != E.running.end();) {

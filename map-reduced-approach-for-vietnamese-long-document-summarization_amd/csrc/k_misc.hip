@@ -31,6 +31,25 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
   }
 }
 
+// Chained decode steps (engine.cpp decode_run): the step's argmax ids become the next
+// step's input ids (an id outside [0, V) -- a failed row, already finished on the host --
+// is fed as 0 so no gather leaves the table), and every position / key count advances by
+// one.  Args blob layout: [ids | positions | slots | key counts], B each.
+__global__ void decode_advance_kernel(int32_t* __restrict__ args, const int32_t* __restrict__ ids_out,
+                                      int B, int V) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const int id = ids_out[b];
+  args[b] = (id >= 0 && id < V) ? id : 0;
+  args[B + b] += 1;
+  args[3 * B + b] += 1;
+}
+
+void launch_decode_advance(int32_t* args, const int32_t* ids_out, int B, int V, hipStream_t s) {
+  if (B <= 0) return;
+  MS_LAUNCH(decode_advance_kernel, dim3((B + 255) / 256), dim3(256), 0, s, args, ids_out, B, V);
+}
+
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
   if (T <= 0) return;
   MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
