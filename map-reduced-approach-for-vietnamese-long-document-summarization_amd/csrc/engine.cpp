@@ -143,7 +143,8 @@ struct ms_engine {
   // kernels' pointers and the step-argument layout depend on nothing else
   std::map<std::pair<int, int>, hipGraphExec_t> decode_graphs;
   bool use_graphs = true;
-  int32_t* ids_host = nullptr;  // pinned ring: kMaxRun steps x max_batch greedy ids
+  int32_t* ids_host = nullptr;  // pinned landing buffer: kMaxRun steps x <= 256 greedy ids
+  int32_t* ids_ring_d = nullptr;  // device ring of a decode run's ids (decode_advance)
   static constexpr int kMaxRun = 64;  // chained decode steps per host synchronisation
   int max_run = kMaxRun;              // MS_DECODE_RUN (1 = one step per ms_step)
 
@@ -553,8 +554,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
-    HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * std::max(cfg->max_batch, 256) * sizeof(int32_t),
+    HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * 256 * sizeof(int32_t),
                          hipHostMallocDefault));
+    E.ids_ring_d = E.dalloc<int32_t>((size_t)ms_engine::kMaxRun * 256);
     if (const char* v = getenv("MS_DECODE_RUN")) E.max_run = std::max(1, std::min(atoi(v), (int)ms_engine::kMaxRun));
     if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
     HIP_OK(hipDeviceSynchronize());
@@ -1046,7 +1048,7 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     E.prof_end(K_MISC);
   }
   // the next chained step's arguments, on the device (decode_run)
-  launch_decode_advance(d, E.ids_out_d, B, E.V, E.stream);
+  launch_decode_advance(d, E.ids_out_d, E.ids_ring_d, B, E.V, E.stream);
 }
 
 // k chained greedy decode steps for every sequence of `batch` (B rows of one token each)
@@ -1066,6 +1068,7 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   for (Seq* s : batch) a.push_back(s->len);         // [B, 2B)  positions
   for (Seq* s : batch) a.push_back(s->slot);        // [2B, 3B) block-table rows
   for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
+  a.push_back(0);                                   // [4B]     step of the run (ring row)
   HIP_OK(hipEventRecord(E.ev_a, E.stream));
   int32_t* d = E.upload_args(a);
   DecodeAttnArgs da;
@@ -1094,10 +1097,10 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
     if (ex) HIP_OK(hipGraphLaunch(ex, E.stream));
     else decode_body(E, B, d, da);
     HIP_OK(hipGetLastError());
-    HIP_OK(hipMemcpyAsync(E.ids_host + (size_t)j * B, E.ids_out_d, B * sizeof(int32_t),
-                          hipMemcpyDeviceToHost, E.stream));
   }
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
+  HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_ring_d, (size_t)k * B * sizeof(int32_t), hipMemcpyDeviceToHost,
+                        E.stream));
   ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
   std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));

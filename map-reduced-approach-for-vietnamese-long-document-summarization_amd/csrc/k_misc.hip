@@ -33,21 +33,30 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
 
 // Chained decode steps (engine.cpp decode_run): the step's argmax ids become the next
 // step's input ids (an id outside [0, V) -- a failed row, already finished on the host --
-// is fed as 0 so no gather leaves the table), and every position / key count advances by
-// one.  Args blob layout: [ids | positions | slots | key counts], B each.
-__global__ void decode_advance_kernel(int32_t* __restrict__ args, const int32_t* __restrict__ ids_out,
-                                      int B, int V) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= B) return;
-  const int id = ids_out[b];
-  args[b] = (id >= 0 && id < V) ? id : 0;
-  args[B + b] += 1;
-  args[3 * B + b] += 1;
+// is fed as 0 so no gather leaves the table), every position / key count advances by one,
+// and the raw ids are appended to the run's device ring at row `step` (args[4B], then
+// incremented), which the host copies back once per run.  Args blob layout:
+// [ids | positions | slots | key counts] (B each) + [step].  One block: B <= 256.
+__global__ __launch_bounds__(256) void decode_advance_kernel(int32_t* __restrict__ args,
+                                                             const int32_t* __restrict__ ids_out,
+                                                             int32_t* __restrict__ ring, int B, int V) {
+  const int b = threadIdx.x;
+  const int step = args[4 * B];
+  if (b < B) {
+    const int id = ids_out[b];
+    ring[(size_t)step * B + b] = id;
+    args[b] = (id >= 0 && id < V) ? id : 0;
+    args[B + b] += 1;
+    args[3 * B + b] += 1;
+  }
+  __syncthreads();  // every thread has read `step`
+  if (b == 0) args[4 * B] = step + 1;
 }
 
-void launch_decode_advance(int32_t* args, const int32_t* ids_out, int B, int V, hipStream_t s) {
-  if (B <= 0) return;
-  MS_LAUNCH(decode_advance_kernel, dim3((B + 255) / 256), dim3(256), 0, s, args, ids_out, B, V);
+void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring, int B, int V,
+                           hipStream_t s) {
+  if (B <= 0 || B > 256) return;  // callers chain sub-batches of <= 256 rows
+  MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
 }
 
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {

@@ -36,8 +36,10 @@ struct DecodeAttnArgs {
 
 void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
 // chained decode: next ids <- this step's argmax (clamped into [0, V)), positions and key
-// counts += 1 in the step-argument blob [ids | positions | slots | key counts]
-void launch_decode_advance(int32_t* args, const int32_t* ids_out, int B, int V, hipStream_t s);
+// counts += 1 in the step-argument blob [ids | positions | slots | key counts | step], and the
+// raw ids appended to ring row `step` (B <= 256)
+void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring, int B, int V,
+                           hipStream_t s);
 void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
                     const int32_t* row_idx, hipStream_t s);
 // RoPE on Q (in place, rope-permuted -> natural dim order) and K; K,V scattered into the
