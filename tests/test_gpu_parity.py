@@ -401,6 +401,31 @@ def test_batch_invariance_large_regime(dev, n_all, n_sub):
         e.close()
 
 
+def test_eos_mid_run_in_a_batch(dev):
+    """A chunk that meets EOS in the middle of a chained decode run stops there (its extra
+    device steps are dropped) while its batch companions run on unchanged: every chunk's
+    result equals its solo run under the same EOS set."""
+    prompts = [_prompt(n, 1700 + n) for n in (30, 90, 150)]
+    e = Engine(TINY, device=0, max_batch=3, max_ctx=512, max_prefill_tokens=1024)
+    try:
+        e.init_synthetic(SEED, STD, JITTER)
+        free = e.generate(prompts[:1], num_predict=24, ignore_eos=True)[0].ids
+    finally:
+        e.close()
+    eos = free[9]
+    e = Engine(TINY, device=0, max_batch=3, max_ctx=512, max_prefill_tokens=1024, eos_ids=(eos,))
+    try:
+        e.init_synthetic(SEED, STD, JITTER)
+        together = e.generate(prompts, num_predict=24)
+        first = free.index(eos)
+        assert together[0].finish == "eos" and together[0].ids == free[:first]
+        for p, r in zip(prompts, together):
+            alone = e.generate([p], num_predict=24)[0]
+            assert (alone.ids, alone.finish) == (r.ids, r.finish)
+    finally:
+        e.close()
+
+
 def test_eos_stops_and_is_dropped(dev, oracle):
     """With the oracle's own first greedy token declared EOS the chunk ends at once,
     empty -- as Ollama drops <|eot_id|> from `response`."""
