@@ -153,7 +153,11 @@ int ms_declare_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggm
 /* ---- request path (replaces one /api/generate per chunk) -------------------- */
 int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict,
               uint32_t flags, uint64_t tag);
-/* one scheduler iteration; returns sequences still waiting or running (>= 0) */
+/* one scheduler iteration: admit + prefill, then a decode run of up to 64 chained greedy
+   steps with one host synchronisation (fewer when a chunk reaches num_predict, the
+   attention split grid changes, or admissible work waits for a slot); a chunk that meets
+   EOS mid-run stops there.  Returns sequences still waiting or running (>= 0).
+   MS_DECODE_RUN=1 in the environment restores one decode step per call. */
 int ms_step(ms_engine* e);
 /* copies up to cap finished results; returns the number copied */
 int ms_poll(ms_engine* e, ms_result* out, int32_t cap);
