@@ -124,7 +124,10 @@ struct ms_engine {
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
   bool large(int) const { return large_engine; }
-  int qsplit = 0;  // >0: split count for every quantised slab projection (MS_QSPLIT); 0: as bf16
+  // split count of every quantised slab projection (MS_QSPLIT; 0: as bf16): 4 measured best
+  // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the bf16 splits (6 / 6 / 4), 2 / 3 / 8
+  // slower (profiles/r02/v27_qsplit_sweep_q4_k_m.txt)
+  int qsplit = 4;
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
   // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
   bool attn_slabs = true, attn_fused_combine = false;
