@@ -23,6 +23,7 @@
 #include <array>
 #include <functional>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -144,7 +145,12 @@ struct ms_engine {
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
   // decode steps replay a captured hipGraph per (batch rows, attention splits): the
   // kernels' pointers and the step-argument layout depend on nothing else
-  std::map<std::pair<int, int>, hipGraphExec_t> decode_graphs;
+  // key: (batch rows, attention split grid, decode steps captured in the graph)
+  std::map<std::tuple<int, int, int>, hipGraphExec_t> decode_graphs;
+  // chained decode steps per graph launch (MS_GRAPH_STEPS): 16 measured 12.12 -> 12.20
+  // chunks/s on configs[1], unchanged on the ragged level and configs[2]
+  // (profiles/r02/v35_graph_steps_ab.txt); a run's remainder uses the one-step graph
+  int graph_steps = 16;
   bool use_graphs = true;
   int32_t* ids_host = nullptr;  // pinned landing buffer: kMaxRun steps x <= 256 greedy ids
   int32_t* ids_ring_d = nullptr;  // device ring of a decode run's ids (decode_advance)
@@ -554,6 +560,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.large_engine = cfg->max_batch >= E.dgemm_min;
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
+    if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
     HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
@@ -1081,26 +1088,29 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   // the split grid only depends on the longest sequence rounded up to 256 keys
   da.max_len = ((max_len + k - 1 + 255) / 256) * 256;
   da.ppw = E.attn_ppw;
-  hipGraphExec_t ex = nullptr;
-  if (E.use_graphs && E.prof_mask == 0) {
-    const auto key = std::make_pair(B, da.max_len);
+  auto graph = [&](int steps) {  // `steps` chained decode bodies in one graph
+    const auto key = std::make_tuple(B, da.max_len, steps);
     auto it = E.decode_graphs.find(key);
     if (it == E.decode_graphs.end()) {
       hipGraph_t g = nullptr;
+      hipGraphExec_t ex = nullptr;
       HIP_OK(hipStreamBeginCapture(E.stream, hipStreamCaptureModeRelaxed));
-      decode_body(E, B, d, da);
+      for (int i = 0; i < steps; ++i) decode_body(E, B, d, da);
       HIP_OK(hipStreamEndCapture(E.stream, &g));
       HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       HIP_OK(hipGraphDestroy(g));
       it = E.decode_graphs.emplace(key, ex).first;
     }
-    ex = it->second;
+    return it->second;
+  };
+  if (E.use_graphs && E.prof_mask == 0) {
+    const int G = std::max(1, E.graph_steps);
+    for (int j = 0; j + G <= k; j += G) HIP_OK(hipGraphLaunch(graph(G), E.stream));
+    for (int j = 0; j < k % G; ++j) HIP_OK(hipGraphLaunch(graph(1), E.stream));
+  } else {
+    for (int j = 0; j < k; ++j) decode_body(E, B, d, da);
   }
-  for (int j = 0; j < k; ++j) {
-    if (ex) HIP_OK(hipGraphLaunch(ex, E.stream));
-    else decode_body(E, B, d, da);
-    HIP_OK(hipGetLastError());
-  }
+  HIP_OK(hipGetLastError());
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
   HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_ring_d, (size_t)k * B * sizeof(int32_t), hipMemcpyDeviceToHost,
                         E.stream));
