@@ -167,6 +167,9 @@ def parse_args(argv=None):
     ap.add_argument("--model", default="llama3.2-3b")
     ap.add_argument("--weights", choices=("bf16", "q4_k_m"), default="bf16",
                     help="q4_k_m = BASELINE configs[4]: random Q4_K/Q6_K blocks, K-quant decode GEMVs")
+    ap.add_argument("--eos", type=int, default=0,
+                    help="natural-EOS mode: stop at a synthetic set of N stop ids (seeded) instead of "
+                         "ignore_eos, so chunks finish at varied lengths and slots turn over")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="skip HIP-event timing of the GEMV class")
     ap.add_argument("--no-check", action="store_true", help="skip the output self-checks")
@@ -226,10 +229,15 @@ def main():
     t_load = time.perf_counter() - t_load
     chunks = [synthetic_chunks(1, args.prompt_len, u.doc, cfg.vocab, cfg.bos_id, first_chunk=u.chunk)[0]
               for u in units]
+    ignore_eos = args.eos <= 0
+    if not ignore_eos:
+        # random-init weights almost never pick the three real end-of-turn ids: a seeded stop set
+        # of N ids ends a chunk with probability ~N/vocab per token (mean length ~vocab/N)
+        eng.set_eos_ids(np.random.default_rng(99).choice(128000, size=args.eos, replace=False))
     gather_s = [0.0]
 
     def one_step():
-        res = eng.generate(chunks, num_predict=args.gen_len, ignore_eos=True)
+        res = eng.generate(chunks, num_predict=args.gen_len, ignore_eos=ignore_eos)
         packed = pack_results(units, [r.ids for r in res], args.gen_len)
         t0 = time.perf_counter()
         rows = gather_summaries(packed, max_rows, device=dev)
@@ -268,8 +276,8 @@ def main():
     check = None
     if not args.no_check:
         same = all(o == outs[0] for o in outs[1:])
-        full = all(len(ids) == args.gen_len for ids in outs[0])
-        alone = eng.generate([chunks[0]], num_predict=args.gen_len, ignore_eos=True)[0].ids
+        full = all(len(ids) == args.gen_len for ids in outs[0]) or not ignore_eos
+        alone = eng.generate([chunks[0]], num_predict=args.gen_len, ignore_eos=ignore_eos)[0].ids
         check = {"deterministic_across_steps": same, "full_length": full,
                  "batch_invariant_chunk0": alone == outs[0][0]}
         assert same and full and check["batch_invariant_chunk0"], check
@@ -320,15 +328,19 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 4), "unit": "chunks/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "q4_k_m+bf16" if quant else "bf16",
         "data": ("synthetic (random Q4_K/Q6_K blocks in the Q4_K_M mix, seed 2, uniform token ids)"
                  if quant else "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)"),
         "config": {"workload": (f"configs[2]: {args.docs} docs x {CHUNKS_PER_DOC} x {args.prompt_len}-tok "
                                 f"chunks over {world} GPU(s) ({n_local} per GPU, <= {B} in flight, "
                                 f"continuous batching)" if args.docs else
                                 f"{'configs[4]' if quant else 'configs[1]'}: {B} x {args.prompt_len}-tok chunks")
-                               + f" -> {args.gen_len}-tok greedy summaries (ignore_eos), batched prefill + "
-                                 f"decode, summary ids gathered to rank 0",
+                               + (f" -> {args.gen_len}-tok greedy summaries (ignore_eos)" if ignore_eos else
+                                  f" -> greedy summaries of <= {args.gen_len} tok stopping at a synthetic "
+                                  f"{args.eos}-id stop set (natural EOS, mean "
+                                  f"{np.mean([len(x) for x in outs[0]]):.1f} tok)")
+                               + ", batched prefill + decode, summary ids gathered to rank 0",
                    "model": cfg.name, "weights": args.weights, "chunks_per_gpu": n_local, "max_batch": B,
                    "prompt_tokens": args.prompt_len, "summary_tokens": args.gen_len,
                    "global_batch": total_chunks // args.steps,
@@ -336,6 +348,8 @@ def main():
         "breakdown": {"prefill_ms_per_step": round(st["prefill_ms"] / args.steps, 2),
                       "decode_ms_per_step": round(st["decode_ms"] / args.steps, 2),
                       "decode_steps": st["decode_steps"],
+                      "summary_tokens_per_step": int(sum(len(x) for x in outs[0])),
+                      "graphs_built": st["graphs_built"],
                       "decode_ms_per_decode_step": round(st["decode_ms"] / max(st["decode_steps"], 1), 4),
                       "gather_ms_per_step": round(gather_s[0] / args.steps * 1e3, 3),
                       "weight_load_s": round(t_load, 3),

@@ -113,6 +113,8 @@ typedef struct ms_stats {
   int64_t kernel_launches[8];
   int64_t decode_kv_tokens;     /* sum over decode steps and rows of the keys attended
                                    (the KV-read term of SURVEY.md §8d's decode bytes)  */
+  int64_t graphs_built;         /* decode hipGraphs captured + instantiated (the cache keeps
+                                   at most 64, least recently used evicted)            */
 } ms_stats;
 
 typedef struct ms_engine ms_engine;
@@ -153,6 +155,10 @@ int ms_declare_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggm
 /* ---- request path (replaces one /api/generate per chunk) -------------------- */
 int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict,
               uint32_t flags, uint64_t tag);
+/* replace the config's end-of-turn ids by a larger stop set (0 <= ids < vocab; n = 0 restores
+   cfg.eos_ids).  Ollama's `stop` option; bench.py --eos uses a synthetic set so that random-init
+   weights finish chunks at natural, varied lengths (slot turnover). */
+int ms_set_eos_ids(ms_engine* e, const int32_t* ids, int32_t n);
 /* one scheduler iteration: admit + prefill, then a decode run of up to 64 chained greedy
    steps with one host synchronisation (fewer when a chunk reaches num_predict, the
    attention split grid changes, or admissible work waits for a slot); a chunk that meets
@@ -174,6 +180,18 @@ int ms_synchronize(ms_engine* e);
    n_layers_run == n_layers). */
 int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run,
                float* hidden_out, float* logits_out);
+/* the same over n_seqs prompts packed into ONE varlen prefill pass (the ragged batches of
+   the hierarchical runner, runners/run_summarization_ollama_mapreduce_hierarchical.py:242-274):
+   ids = the prompts back to back, lens[i] = length of prompt i; hidden_out / logits_out rows
+   follow the packed order ([sum lens][hidden], [sum lens][vocab]). */
+int ms_forward_packed(ms_engine* e, const int32_t* ids, const int32_t* lens, int32_t n_seqs,
+                      int32_t n_layers_run, float* hidden_out, float* logits_out);
+/* teacher forcing through the DECODE path (parity tests): as ms_submit, but decode step j
+   (j >= 1) is fed forced[j-1] instead of the engine's own previous choice, so the result ids
+   are the engine's greedy choices after a context the caller fixes (e.g. the oracle's own
+   greedy tokens).  n_forced >= num_predict - 1.  Such a sequence decodes one step per run. */
+int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t* forced,
+                     int32_t n_forced, int32_t num_predict, uint32_t flags, uint64_t tag);
 
 /* ---- op-level entry points (device pointers; stream = hipStream_t or NULL) -- */
 #define MS_EPI_STORE_BF16 0  /* out bf16 [M][ldo]                              */
@@ -195,6 +213,9 @@ int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, in
 /* tuning hook: as ms_op_gemv with the K-splitting wave count forced (0 = heuristic) */
 int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                      int32_t ldo, int32_t epilogue, void* workspace, int32_t waves, void* stream);
+/* tuning hook: ms_op_gemv over X [M][ldk] and W [N][ldk] (row stride ldk >= K elements) */
+int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+                       int32_t ldk, int32_t ldo, int32_t epilogue, void* stream);
 /* large-batch decode GEMM (M <= 256 rows; 64 weight rows per block, X shared via LDS): the
    ms_op_gemv epilogues (plus MS_EPI_ARGMAX); S > 1: split-K fp32 slabs [S][M][N] with
    epilogue MS_EPI_STORE_F32; N % 64 == 0, K % (64 S) == 0 */

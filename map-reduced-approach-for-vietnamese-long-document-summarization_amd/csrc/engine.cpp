@@ -67,6 +67,10 @@ struct Seq {
   std::vector<int32_t> out;
   std::vector<int32_t> pages;
   int finish = 0;
+  // teacher forcing (ms_submit_forced, parity tests): decode step j is fed forced[j-1]
+  // instead of the sequence's own previous choice; `out` keeps the engine's choices
+  std::vector<int32_t> forced;
+  int32_t next_input() const { return forced.empty() ? out.back() : forced[out.size() - 1]; }
 };
 
 struct Layer {
@@ -124,6 +128,18 @@ struct ms_engine {
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
+  // norm-fused decode (engines of <= kNormMaxBatch slots, bf16 weights; MS_NORM_FUSED=0 turns it
+  // off): no residual_rmsnorm launches -- O and down run unsplit on norm_rt-row tiles (3072 / 12
+  // = 256 workgroups) and add into the fp32 residual themselves, writing per-tile sums of squares
+  // (ssq [tiles][B]); QKV and gate/up build their X as bf16(rmsnorm(x) * g) in their own
+  // prologue from those sums (k_gemv.hip kXNorm).  Chosen per engine, like the regimes above.
+  bool norm_fuse = true, has_quant = false;
+  int norm_rt = 12, ssq_tiles = 0;
+  float* ssq = nullptr;
+  static constexpr int kNormMaxBatch = 10;
+  bool norm_fused() const {
+    return norm_fuse && !has_quant && !large_engine && cfg.max_batch <= kNormMaxBatch && attn_slabs;
+  }
   bool large(int) const { return large_engine; }
   // split count of every quantised slab projection (MS_QSPLIT; 0: as bf16): 4 measured best
   // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the bf16 splits (6 / 6 / 4), 2 / 3 / 8
@@ -135,6 +151,7 @@ struct ms_engine {
   int32_t* args_d = nullptr;
   int32_t* args_h = nullptr;  // pinned
   size_t args_cap = 0;
+  std::vector<uint8_t> stop_set;  // ms_set_eos_ids: a stop-id bitmap replacing cfg.eos_ids
   std::deque<std::unique_ptr<Seq>> waiting;
   std::vector<std::unique_ptr<Seq>> running;
   std::vector<std::unique_ptr<Seq>> done, polled;
@@ -146,7 +163,11 @@ struct ms_engine {
   // decode steps replay a captured hipGraph per (batch rows, attention splits): the
   // kernels' pointers and the step-argument layout depend on nothing else
   // key: (batch rows, attention split grid, decode steps captured in the graph)
-  std::map<std::tuple<int, int, int>, hipGraphExec_t> decode_graphs;
+  // (graph, last use) -- least recently used graphs are destroyed beyond kMaxGraphs, so ragged
+  // or admission-ramp workloads with many distinct (B, length bucket) keys stay bounded
+  std::map<std::tuple<int, int, int>, std::pair<hipGraphExec_t, uint64_t>> decode_graphs;
+  uint64_t graph_clock = 0;
+  static constexpr size_t kMaxGraphs = 64;
   // chained decode steps per graph launch (MS_GRAPH_STEPS): 16 measured 12.12 -> 12.20
   // chunks/s on configs[1], unchanged on the ragged level and configs[2]
   // (profiles/r02/v35_graph_steps_ab.txt); a run's remainder uses the one-step graph
@@ -286,8 +307,53 @@ struct ms_engine {
     pending_split = 0;
   }
 
+  GemvArgs norm_args(const bf16_t* gamma) const {
+    GemvArgs g{};
+    g.xres = x;
+    g.ssq_in = ssq;
+    g.ssq_tiles = ssq_tiles;
+    g.gamma = gamma;
+    g.hdim = H;
+    g.eps = cfg.norm_eps;
+    return g;
+  }
+
+  // one layer of the norm-fused decode step (norm_fused()): 5 launches instead of 7
+  void run_layer_norm_fused(int l, int B, const DecodeAttnArgs& da) {
+    const Layer& Ly = layers[l];
+    KVView kv = kv_layer(l);
+    // QKV -> split-K slabs; each block normalises its slice of x with attn_norm first
+    GemvArgs gq = norm_args(Ly.attn_norm);
+    prof_begin(K_GEMV);
+    launch_gemv_split(xb, Ly.wqkv, slabs, B, QKVN, H, split_qkv, 0, stream, &gq);
+    prof_end(K_GEMV);
+    DecodeQKV qa{nullptr, slabs, split_qkv, cos_tab, sin_tab};
+    prof_begin(K_ATTN_DECODE);
+    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
+    prof_end(K_ATTN_DECODE);
+    // O: x += attn . Wo^T on norm_rt-row tiles, + the ffn norm's statistics
+    GemvArgs go{};
+    go.rt = norm_rt;
+    go.ssq_out = ssq;
+    prof_begin(K_GEMV);
+    launch_gemv_ex(attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_RESID_SSQ, &go, 0, stream);
+    prof_end(K_GEMV);
+    ssq_tiles = (H + norm_rt - 1) / norm_rt;
+    GemvArgs gg = norm_args(Ly.ffn_norm);
+    prof_begin(K_GEMV);
+    launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, 0, stream);
+    prof_end(K_GEMV);
+    prof_begin(K_GEMV);
+    launch_gemv_ex(hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_RESID_SSQ, &go, 0, stream);
+    prof_end(K_GEMV);
+  }
+
   void run_layer_fused_decode(int l, int B, const int32_t* tok_pos, const int32_t* tok_slot,
                               const DecodeAttnArgs& da) {
+    if (norm_fused()) {
+      run_layer_norm_fused(l, B, da);
+      return;
+    }
     const Layer& Ly = layers[l];
     KVView kv = kv_layer(l);
     residual_norm(Ly.attn_norm, B);
@@ -398,8 +464,17 @@ struct ms_engine {
   // Captured decode graphs bake in the weight form (bf16 vs K-quant stream) and the split
   // choices: any weight (re)load invalidates them.
   void drop_graphs() {
-    for (auto& kv : decode_graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
     decode_graphs.clear();
+  }
+  void evict_graphs() {  // keep at most kMaxGraphs - 1 before inserting one more
+    while (decode_graphs.size() >= kMaxGraphs) {
+      auto lru = decode_graphs.begin();
+      for (auto it = decode_graphs.begin(); it != decode_graphs.end(); ++it)
+        if (it->second.second < lru->second.second) lru = it;
+      (void)hipGraphExecDestroy(lru->second.first);
+      decode_graphs.erase(lru);
+    }
   }
 
   int32_t* upload_args(const std::vector<int32_t>& a) {
@@ -560,6 +635,14 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.large_engine = cfg->max_batch >= E.dgemm_min;
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
+    if (const char* v = getenv("MS_NORM_FUSED")) E.norm_fuse = atoi(v) != 0;
+    if (E.H % E.norm_rt || E.H / E.norm_rt > 256) E.norm_rt = 16;
+    E.norm_fuse = E.norm_fuse && E.H % E.norm_rt == 0 && E.H / E.norm_rt <= 256 &&
+                  gemv_norm_supported(cfg->max_batch, E.QKVN, E.H / E.split_qkv, MS_GEMV_EPI_STORE_F32,
+                                      256, 0) &&
+                  gemv_norm_supported(cfg->max_batch, 2 * E.F, E.H, MS_GEMV_EPI_SWIGLU, 256, 0) &&
+                  E.H % E.split_qkv == 0;
+    E.ssq = E.dalloc<float>((size_t)256 * std::max(cfg->max_batch, 16), true);
     if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
     E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
     E.args_d = E.dalloc<int32_t>(E.args_cap);
@@ -587,7 +670,7 @@ int ms_destroy(ms_engine* e) {
   for (void* p : e->allocs) (void)hipFree(p);
   if (e->args_h) (void)hipHostFree(e->args_h);
   if (e->ids_host) (void)hipHostFree(e->ids_host);
-  for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
   for (auto& pe : e->ev_pairs) {
     (void)hipEventDestroy(pe.start);
     (void)hipEventDestroy(pe.stop);
@@ -710,6 +793,7 @@ static void load_quant(ms_engine& E, int tensor, int layer, int type, const uint
   uint8_t* q = t.qs ? q_region(E, *t.qs, t.qregion, t.qrow0, t.qrows, type, t.cols) : nullptr;
   launch_quant_rows(type, dblocks, t.rows, t.cols, t.dst, t.mul, t.add, q, t.qrow0, E.stream);
   HIP_OK(hipGetLastError());
+  E.has_quant = true;  // the K-quant decode GEMVs have no norm prologue: the unfused step
   if (t.qs) {
     t.qs->loaded |= (uint32_t)t.qbit;
     t.qs->need = (uint32_t)t.qneed;
@@ -755,6 +839,7 @@ int ms_declare_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t typ
     HIP_OK(hipSetDevice(E.cfg.device));
     TensorDst t = tensor_dst(E, tensor, layer);
     REQUIRE(t.rows > 1 && t.cols % 256 == 0, MS_EINVAL, "not a K-quant matrix");
+    E.has_quant = true;
     if (t.qs) {  // the layout of a quantised load, without its bytes (a broadcast fills them)
       q_region(E, *t.qs, t.qregion, t.qrow0, t.qrows, type, t.cols);
       t.qs->loaded |= (uint32_t)t.qbit;
@@ -865,27 +950,49 @@ int ms_init_synthetic(ms_engine* e, uint64_t seed, float std_, float jitter) {
   });
 }
 
+static void submit_seq(ms_engine& E, const int32_t* ids, int32_t n, int32_t num_predict, uint32_t flags,
+                       uint64_t tag, const int32_t* forced, int32_t n_forced) {
+  REQUIRE(ids != nullptr && n >= 1, MS_EINVAL, "empty prompt");
+  REQUIRE(num_predict >= 1, MS_EINVAL, "num_predict must be >= 1");
+  REQUIRE((int64_t)n + num_predict <= E.cfg.max_ctx, MS_ENOSPC,
+          "prompt (" + std::to_string(n) + ") + num_predict (" + std::to_string(num_predict) +
+              ") exceeds max_ctx " + std::to_string(E.cfg.max_ctx));
+  REQUIRE(n <= E.cfg.max_prefill_tokens, MS_ENOSPC, "prompt longer than max_prefill_tokens");
+  const int need = (n + num_predict + kPage - 1) / kPage;
+  REQUIRE(need <= E.n_pages, MS_ENOSPC, "request needs more KV pages than the pool holds");
+  for (int i = 0; i < n; ++i)
+    REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range at position " + std::to_string(i));
+  auto s = std::make_unique<Seq>();
+  if (forced) {
+    REQUIRE(n_forced >= num_predict - 1, MS_EINVAL, "teacher forcing needs num_predict - 1 forced ids");
+    for (int i = 0; i < num_predict - 1; ++i)
+      REQUIRE(forced[i] >= 0 && forced[i] < E.V, MS_EINVAL, "forced id out of range at " + std::to_string(i));
+    s->forced.assign(forced, forced + std::max(num_predict - 1, 0));
+    s->forced.push_back(0);  // never fed: the last step's choice ends the sequence
+  }
+  s->tag = tag;
+  s->prompt.assign(ids, ids + n);
+  s->num_predict = num_predict;
+  s->flags = flags;
+  E.waiting.push_back(std::move(s));
+}
+
 int ms_submit(ms_engine* e, const int32_t* ids, int32_t n, int32_t num_predict, uint32_t flags,
               uint64_t tag) {
   if (!e) return MS_EINVAL;
   return guarded(e, [&]() -> int {
-    ms_engine& E = *e;
-    REQUIRE(ids != nullptr && n >= 1, MS_EINVAL, "empty prompt");
-    REQUIRE(num_predict >= 1, MS_EINVAL, "num_predict must be >= 1");
-    REQUIRE((int64_t)n + num_predict <= E.cfg.max_ctx, MS_ENOSPC,
-            "prompt (" + std::to_string(n) + ") + num_predict (" + std::to_string(num_predict) +
-                ") exceeds max_ctx " + std::to_string(E.cfg.max_ctx));
-    REQUIRE(n <= E.cfg.max_prefill_tokens, MS_ENOSPC, "prompt longer than max_prefill_tokens");
-    const int need = (n + num_predict + kPage - 1) / kPage;
-    REQUIRE(need <= E.n_pages, MS_ENOSPC, "request needs more KV pages than the pool holds");
-    for (int i = 0; i < n; ++i)
-      REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range at position " + std::to_string(i));
-    auto s = std::make_unique<Seq>();
-    s->tag = tag;
-    s->prompt.assign(ids, ids + n);
-    s->num_predict = num_predict;
-    s->flags = flags;
-    E.waiting.push_back(std::move(s));
+    submit_seq(*e, ids, n, num_predict, flags, tag, nullptr, 0);
+    return MS_OK;
+  });
+}
+
+int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t* forced, int32_t n_forced,
+                     int32_t num_predict, uint32_t flags, uint64_t tag) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    REQUIRE(forced != nullptr || num_predict == 1, MS_EINVAL, "null forced ids");
+    static const int32_t none = 0;
+    submit_seq(*e, ids, n, num_predict, flags, tag, forced ? forced : &none, n_forced);
     return MS_OK;
   });
 }
@@ -896,9 +1003,28 @@ int ms_pending(const ms_engine* e) {
 }
 
 static bool is_eos(const ms_engine& E, int32_t t) {
+  if (!E.stop_set.empty()) return t >= 0 && t < (int)E.stop_set.size() && E.stop_set[t];
   for (int i = 0; i < E.cfg.n_eos; ++i)
     if (E.cfg.eos_ids[i] == t) return true;
   return false;
+}
+
+int ms_set_eos_ids(ms_engine* e, const int32_t* ids, int32_t n) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    REQUIRE(n >= 0 && (n == 0 || ids), MS_EINVAL, "bad stop-id list");
+    std::vector<uint8_t> set;
+    if (n > 0) {
+      set.assign(E.V, 0);
+      for (int i = 0; i < n; ++i) {
+        REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "stop id out of range");
+        set[ids[i]] = 1;
+      }
+    }
+    E.stop_set.swap(set);  // empty: back to the config's eos_ids
+    return MS_OK;
+  });
 }
 
 // returns true if the sequence finished with this token
@@ -1031,8 +1157,10 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   // in-launch split-combine counters start at zero every step (a memset node)
   if (E.attn_fused_combine) HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
   E.prof_begin(K_MISC);
-  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
+  const bool nf = E.norm_fused() && E.fused_decode(B);
+  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream, nf ? E.ssq : nullptr);
   E.prof_end(K_MISC);
+  E.ssq_tiles = 1;  // the embedding's per-row sums of squares
   E.pending_split = 0;
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   E.residual_norm(E.final_norm, B);  // folds the last layer's down slabs (if fused)
@@ -1074,7 +1202,7 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   std::vector<int32_t> a;
   a.reserve(4 * B);
   int max_len = 0;
-  for (Seq* s : batch) a.push_back(s->out.back());  // [0, B)   token ids
+  for (Seq* s : batch) a.push_back(s->next_input());  // [0, B)   token ids
   for (Seq* s : batch) a.push_back(s->len);         // [B, 2B)  positions
   for (Seq* s : batch) a.push_back(s->slot);        // [2B, 3B) block-table rows
   for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
@@ -1092,6 +1220,7 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
     const auto key = std::make_tuple(B, da.max_len, steps);
     auto it = E.decode_graphs.find(key);
     if (it == E.decode_graphs.end()) {
+      E.evict_graphs();
       hipGraph_t g = nullptr;
       hipGraphExec_t ex = nullptr;
       HIP_OK(hipStreamBeginCapture(E.stream, hipStreamCaptureModeRelaxed));
@@ -1099,9 +1228,11 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
       HIP_OK(hipStreamEndCapture(E.stream, &g));
       HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
       HIP_OK(hipGraphDestroy(g));
-      it = E.decode_graphs.emplace(key, ex).first;
+      it = E.decode_graphs.emplace(key, std::make_pair(ex, (uint64_t)0)).first;
+      E.stats.graphs_built += 1;
     }
-    return it->second;
+    it->second.second = ++E.graph_clock;
+    return it->second.first;
   };
   if (E.use_graphs && E.prof_mask == 0) {
     const int G = std::max(1, E.graph_steps);
@@ -1166,9 +1297,13 @@ int ms_step(ms_engine* e) {
     for (size_t i0 = 0; i0 < batch.size(); i0 += 256) {
       std::vector<Seq*> sub(batch.begin() + i0, batch.begin() + std::min(batch.size(), i0 + 256));
       int k = (batch.size() > 256 || (!E.waiting.empty() && !E.free_slots.empty())) ? 1 : E.max_run;
+      // chunks wait for a slot: a chunk that stops at EOS inside the run keeps its slot until
+      // the run ends, so bound the run by one captured graph (<= 16 steps) instead of 64
+      if (!E.waiting.empty()) k = std::min(k, std::max(1, E.graph_steps));
       int max_len = 0;
       for (Seq* s : sub) {
         k = std::min(k, s->num_predict - (int)s->out.size());
+        if (!s->forced.empty()) k = 1;  // the next input is the forced id, not this step's choice
         max_len = std::max(max_len, s->len + 1);
       }
       k = std::max(1, std::min(k, ((max_len + 255) / 256) * 256 - max_len + 1));
@@ -1252,45 +1387,60 @@ int ms_synchronize(ms_engine* e) {
   });
 }
 
-int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run, float* hidden_out,
-               float* logits_out) {
+int ms_forward_packed(ms_engine* e, const int32_t* ids, const int32_t* lens, int32_t n_seqs,
+                      int32_t n_layers_run, float* hidden_out, float* logits_out) {
   if (!e) return MS_EINVAL;
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     HIP_OK(hipSetDevice(E.cfg.device));
     REQUIRE(E.waiting.empty() && E.running.empty(), MS_EBUSY, "ms_forward needs an idle engine");
-    REQUIRE(ids && n >= 1 && n <= E.cfg.max_prefill_tokens && n <= E.cfg.max_ctx, MS_EINVAL, "bad probe length");
+    REQUIRE(ids && lens && n_seqs >= 1 && n_seqs <= (int)E.free_slots.size(), MS_EINVAL,
+            "bad probe batch (1 <= n_seqs <= max_batch)");
     REQUIRE(n_layers_run >= 0 && n_layers_run <= E.L, MS_EINVAL, "n_layers_run out of range");
     REQUIRE(!logits_out || n_layers_run == E.L, MS_EINVAL, "logits need every layer");
-    REQUIRE((n + kPage - 1) / kPage <= (int)E.free_pages.size(), MS_ENOSPC, "not enough KV pages");
-    for (int i = 0; i < n; ++i) REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range");
-    Seq s;
-    s.prompt.assign(ids, ids + n);
-    reserve(E, s, n);
-    std::vector<Seq*> b{&s};
+    int64_t T = 0, pages = 0;
+    for (int i = 0; i < n_seqs; ++i) {
+      REQUIRE(lens[i] >= 1 && lens[i] <= E.cfg.max_ctx, MS_EINVAL, "bad probe length");
+      T += lens[i];
+      pages += (lens[i] + kPage - 1) / kPage;
+    }
+    REQUIRE(T <= E.cfg.max_prefill_tokens, MS_EINVAL, "probe longer than max_prefill_tokens");
+    REQUIRE(pages <= (int64_t)E.free_pages.size(), MS_ENOSPC, "not enough KV pages");
+    for (int64_t i = 0; i < T; ++i) REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range");
+    std::vector<Seq> seqs(n_seqs);
+    std::vector<Seq*> b;
+    int64_t off = 0;
+    for (int i = 0; i < n_seqs; ++i) {
+      seqs[i].prompt.assign(ids + off, ids + off + lens[i]);
+      off += lens[i];
+      reserve(E, seqs[i], lens[i]);
+      b.push_back(&seqs[i]);
+    }
     float* lg = nullptr;
-    int rc = MS_OK;
     try {
-      if (logits_out) {
-        HIP_OK(hipMalloc((void**)&lg, (size_t)n * E.V * sizeof(float)));
-      }
+      if (logits_out) HIP_OK(hipMalloc((void**)&lg, (size_t)T * E.V * sizeof(float)));
       prefill(E, b, n_layers_run, lg, nullptr);
       HIP_OK(hipStreamSynchronize(E.stream));
       if (hidden_out)
-        HIP_OK(hipMemcpy(hidden_out, E.x, (size_t)n * E.H * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(hidden_out, E.x, (size_t)T * E.H * sizeof(float), hipMemcpyDeviceToHost));
       if (logits_out)
-        HIP_OK(hipMemcpy(logits_out, lg, (size_t)n * E.V * sizeof(float), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(logits_out, lg, (size_t)T * E.V * sizeof(float), hipMemcpyDeviceToHost));
     } catch (...) {
       if (lg) (void)hipFree(lg);
-      release(E, s);
+      for (Seq& s : seqs) release(E, s);
       throw;
     }
     if (lg) (void)hipFree(lg);
-    release(E, s);
+    for (Seq& s : seqs) release(E, s);
     E.ev_pending.clear();
     E.ev_used = 0;
-    return rc;
+    return MS_OK;
   });
+}
+
+int ms_forward(ms_engine* e, const int32_t* ids, int32_t n, int32_t n_layers_run, float* hidden_out,
+               float* logits_out) {
+  return ms_forward_packed(e, ids, &n, 1, n_layers_run, hidden_out, logits_out);
 }
 
 // ---------------------------------------------------------------------------- op entry points
@@ -1343,6 +1493,17 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
     launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
                    (hipStream_t)stream);
+  });
+}
+
+int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
+                       int32_t ldk, int32_t ldo, int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && W && out && N >= 16 && N % 16 == 0 && ldk >= K && ldk % 8 == 0, MS_EINVAL,
+            "bad strided gemv operands");
+    REQUIRE(epi >= 0 && epi <= 3 && epi != MS_EPI_SWIGLU, MS_EINVAL, "bad epilogue");
+    REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported");
+    launch_gemv_strided((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldk, ldo, epi, (hipStream_t)stream);
   });
 }
 

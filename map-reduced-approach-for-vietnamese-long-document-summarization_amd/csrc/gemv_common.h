@@ -54,8 +54,67 @@ __device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict_
   }
 }
 
-// where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip)
-enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
+// where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip);
+// kXNorm: the LDS image of bf16(rmsnorm(x) * gamma), built by the block itself (gemv_norm_x)
+enum { kXGlobal = 0, kXLds = 1, kXRegs = 2, kXNorm = 3 };
+constexpr int kNormChunks = 4;  // float4 chunks of x per thread and pass (kXNorm prologue)
+
+// The RMSNorm of the decode step, folded into the GEMV that consumes it (no norm launch):
+// xn[r][k] = bf16((x[r][k] * rinv[r]) * gamma[k]) for the block's K slice [k0, k0+K), written
+// into the X LDS image (x_lds layout), rinv[r] = 1/sqrt(sum_t ssq[t][r] / hdim + eps) from the
+// per-tile sums of squares of the RESID_SSQ producer.  Summation order is fixed (per lane
+// t = lane, +64, +128, +192 in sequence, then the wave tree) and per row, so a row's norm does
+// not depend on M or on the other rows.  Runs before the weight stream, in passes of
+// kNormChunks float4 per thread (the first pass's loads issued ahead of the statistics), so it
+// adds no registers to the GEMV body.  Needs ssq_tiles <= 256.
+__device__ __forceinline__ void gemv_norm_x(char* smem, const GemvArgs& ga, int M, int K, int k0) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int nth = blockDim.x, KC = K >> 2, nch = M * KC;
+  float* rinv = (float*)(smem + gemv_x_lds_bytes(M, K));
+  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+  f32x4 xv[kNormChunks];
+  u32x2 gv[kNormChunks];
+  auto load = [&](int base) {
+#pragma unroll
+    for (int i = 0; i < kNormChunks; ++i) {
+      const int c = min(base + tid + i * nth, nch - 1);
+      const int r = c / KC, cc = c - r * KC;
+      xv[i] = *(const f32x4*)(ga.xres + (size_t)r * ga.hdim + k0 + 4 * cc);
+      gv[i] = *(const u32x2*)(ga.gamma + k0 + 4 * cc);
+    }
+  };
+  load(0);
+  for (int r = wave; r < M; r += nw) {
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = lane + 64 * i;
+      v[i] = t < ga.ssq_tiles ? ga.ssq_in[(size_t)t * M + r] : 0.f;
+    }
+    const float sum = wave_sum(((v[0] + v[1]) + v[2]) + v[3]);
+    if (lane == 0) rinv[r] = 1.0f / sqrtf(sum / (float)ga.hdim + ga.eps);
+  }
+  __syncthreads();
+  for (int base = 0; base < nch; base += kNormChunks * nth) {
+    if (base > 0) load(base);
+#pragma unroll
+    for (int i = 0; i < kNormChunks; ++i) {
+      const int c = base + tid + i * nth;
+      if (c < nch) {
+        const int r = c / KC, cc = c - r * KC;
+        const float ri = rinv[r];
+        const float g0 = __uint_as_float(gv[i].x << 16), g1 = __uint_as_float(gv[i].x & 0xFFFF0000u);
+        const float g2 = __uint_as_float(gv[i].y << 16), g3 = __uint_as_float(gv[i].y & 0xFFFF0000u);
+        uint2 o;
+        o.x = pack2bf((xv[i].x * ri) * g0, (xv[i].y * ri) * g1);
+        o.y = pack2bf((xv[i].z * ri) * g2, (xv[i].w * ri) * g3);
+        *(uint2*)(smem + x_lds(r, 4 * cc, K) + (cc & 1) * 8) = o;
+      }
+    }
+  }
+  __syncthreads();
+}
+
 constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave may hold (<= 32 VGPRs)
 // X source per GEMV family, measured same-box on MI355X at B = 8 (profiles/r02/v14_x_regs_ab.txt):
 // the K-quant GEMVs take X into registers (Q4_K_M decode 2.023 -> 1.950 ms/step: the dequant
@@ -152,6 +211,24 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
             f2bf(sum_e(e_of(row, c)));
       }
     }
+  } else if constexpr (EPI == MS_GEMV_EPI_RESID_SSQ) {
+    static_assert(NT == 1, "residual epilogue works on single-column-tile plans");
+    const int rtv = ga.rt > 0 ? ga.rt : 16;
+    // a row's 16 columns sit in lanes 4c + j of one wave: reduce over lane bits 2..5
+    for (int e = tid; e < ELEMS; e += nthreads) {
+      const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
+      const int row = m * 16 + 4 * (l >> 4) + j, c = l & 15, col = n0 + c;
+      float q = 0.f;
+      if (row < M && c < rtv && col < N) {
+        float* px = (float*)out + (size_t)row * ldo + col;
+        const float xo = *px + sum_e(e);
+        *px = xo;
+        q = xo * xo;
+      }
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
+      if (c == 0 && row < M) ga.ssq_out[(size_t)blockIdx.x * M + row] = q;
+    }
   } else if constexpr (EPI == MS_GEMV_EPI_ARGMAX) {
     static_assert(NT == 1, "argmax epilogue works on 16-column tiles");
     // lanes sharing (m, l>>4, j) hold one row's 16 columns: they differ in lane bits 2..5
@@ -172,7 +249,7 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
       const int m = mn / NT, n = mn % NT;
       const int row = m * 16 + 4 * (l >> 4) + j;
       const int col = n0 + n * 16 + (l & 15);
-      if (row >= M || col >= N) continue;
+      if (row >= M || col >= N || (NT == 1 && ga.rt > 0 && (l & 15) >= ga.rt)) continue;
       const float v = sum_e(e);
       const size_t o = (size_t)row * ldo + col;
       if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v);

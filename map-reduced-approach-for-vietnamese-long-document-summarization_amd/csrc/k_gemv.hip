@@ -31,11 +31,12 @@ struct GemvPlan {
   int MT, NT, waves, U, tiles;
 };
 
-static GemvPlan gemv_plan(int M, int N, int K, int epi, int force_waves = 0) {
+static GemvPlan gemv_plan(int M, int N, int K, int epi, int force_waves = 0, int rt = 0) {
   GemvPlan p;
   p.MT = (M + 15) / 16;
   p.NT = (epi == MS_GEMV_EPI_SWIGLU) ? 2 : 1;
-  p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
+  const int rows = p.NT == 1 && rt > 0 ? rt : 16 * p.NT;
+  p.tiles = (N + rows - 1) / rows;
   const int steps = K / 64;
   int best_w = 0;
   if (force_waves > 0 && steps % force_waves == 0 && steps / force_waves <= 8) {
@@ -58,7 +59,7 @@ constexpr size_t kMaxLds = 160 * 1024;
 // staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of a
 // fragment read on different banks); rows >= M alias row M-1 and are never stored.
 static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
-  size_t xs = xlds ? gemv_x_lds_bytes(M, K) : 0;
+  size_t xs = xlds ? gemv_x_lds_bytes(M, K) + 64 : 0;  // + kXNorm's per-row 1/rms
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;  // per-wave partials
   return xs > red ? xs : red;
 }
@@ -72,15 +73,18 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
 //   kXRegs:   each wave loads its OWN k-slice of X (the only part it multiplies) straight
 //             into registers ahead of its weight loads -- no LDS image, no block barrier,
 //             every wave starts its MFMAs as soon as its own bytes have landed.
+// kXNorm: two 1024-thread blocks per CU (<= 64 VGPRs), as the plain gate/up GEMV gets
 template <int MT, int NT, int EPI, int U, int XM>
-__global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
+__global__ __launch_bounds__(1024, (XM == kXNorm && U <= 4) ? 8 : 1) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
                                                     int ldk, int ldo, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const int n0 = blockIdx.x * 16 * NT;
+  // NT = 1: ga.rt weight rows per tile (lanes fr >= rt duplicate the last row; never stored)
+  const int rt = NT == 1 && ga.rt > 0 ? ga.rt : 16;
+  const int n0 = blockIdx.x * (NT == 1 ? rt : 16 * NT);
   const int kbeg = wave * U * 64;
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
     X += (size_t)blockIdx.y * K;
@@ -88,9 +92,11 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
   }
 
-  // 1. X first (LDS DMA of the block's rows, or this wave's slice into registers), then
-  // this wave's whole W stream: vmcnt retires in issue order
+  // 1. X first (LDS DMA of the block's rows, this wave's slice into registers, or the
+  // RMSNorm of the fp32 residual built in LDS), then this wave's whole W stream: vmcnt
+  // retires in issue order
   if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
+  if constexpr (XM == kXNorm) gemv_norm_x(smem, ga, M, K, blockIdx.y * K);
   uint4 xr[XM == kXRegs ? U : 1][XM == kXRegs ? MT : 1][2];
   if constexpr (XM == kXRegs) {
 #pragma unroll
@@ -106,7 +112,8 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
   uint4 w[U][NT][2];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
-    const bf16_t* wp = W + (size_t)min(n0 + n * 16 + fr, N - 1) * ldk + kbeg + 16 * fg;
+    const int wrow = NT == 1 ? n0 + min(fr, rt - 1) : n0 + n * 16 + fr;
+    const bf16_t* wp = W + (size_t)min(wrow, N - 1) * ldk + kbeg + 16 * fg;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       w[u][n][0] = ldw16(wp + u * 64);
@@ -134,7 +141,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       if constexpr (XM == kXRegs) {
         x0 = as_bf16x8(xr[u][m][0]);
         x1 = as_bf16x8(xr[u][m][1]);
-      } else if constexpr (XM == kXLds) {
+      } else if constexpr (XM == kXLds || XM == kXNorm) {
         const int k0 = kbeg + u * 64 + 16 * fg;
         x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
         x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
@@ -164,6 +171,13 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
     if constexpr (MT * U <= kXRegsMaxFrags) {
       if (xm == kXRegs) {
         MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXRegs>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+                  ldo, ga);
+        return;
+      }
+    }
+    if constexpr (MT == 1) {
+      if (xm == kXNorm) {
+        MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXNorm>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
                   ldo, ga);
         return;
       }
@@ -206,6 +220,7 @@ static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N
     case MS_GEMV_EPI_SWIGLU: GE(2, MS_GEMV_EPI_SWIGLU); break;
     case MS_GEMV_EPI_ROPE_KV: GE(1, MS_GEMV_EPI_ROPE_KV); break;
     case MS_GEMV_EPI_ARGMAX: GE(1, MS_GEMV_EPI_ARGMAX); break;
+    case MS_GEMV_EPI_RESID_SSQ: GE(1, MS_GEMV_EPI_RESID_SSQ); break;
     default: GE(1, MS_GEMV_EPI_STORE_F32); break;
   }
 #undef GE
@@ -221,15 +236,30 @@ bool gemv_supported(int M, int N, int K, int epi) {
   return gemv_lds_bytes(p, M, K, false) <= kMaxLds;
 }
 
+// the kXNorm prologue's limits (gemv_norm_x): one 16-row MFMA tile of X rows, the block's
+// x slice in <= kNormChunks float4 per thread, <= 256 producer tiles, the image in LDS
+bool gemv_norm_supported(int M, int N, int K, int epi, int ssq_tiles, int rt) {
+  if (M < 1 || M > 16 || K % 64 || ssq_tiles < 1 || ssq_tiles > 256) return false;
+  if (epi == MS_GEMV_EPI_ROPE_KV || epi == MS_GEMV_EPI_ARGMAX) return false;
+  const GemvPlan p = gemv_plan(M, N, K, epi, 0, rt);
+  if (p.waves == 0) return false;
+  return gemv_lds_bytes(p, M, K, true) <= kMaxLds;
+}
+
 static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
                           int S, int ldo, int epi, const GemvArgs* ga_in, int force_waves,
                           hipStream_t s) {
   if (M <= 0) return;
-  const GemvPlan p = gemv_plan(M, N, K, epi, force_waves);
+  const int rt = ga_in ? ga_in->rt : 0;
+  const GemvPlan p = gemv_plan(M, N, K, epi, force_waves, rt);
   if (p.waves == 0) return;  // callers check gemv_supported()
   const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
   int xm = xl ? kXLds : kXGlobal;
   if (gemv_x_regs() && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
+  if (ga_in && ga_in->xres) {
+    if (!gemv_norm_supported(M, N, K, epi, ga_in->ssq_tiles, rt)) return;  // callers check
+    xm = kXNorm;
+  }
   const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds);
   if (lds > kMaxLds) return;
   GemvArgs ga{};
@@ -247,14 +277,20 @@ void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
   gemv_dispatch(X, W, out, M, N, K, K, 1, ldo, epi, ga_in, force_waves, s);
 }
 
+// tuning hook: W rows of stride ldk >= K elements (padded layouts: HBM channel spread)
+void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                         int ldo, int epi, hipStream_t s) {
+  gemv_dispatch(X, W, out, M, N, K, ldk, 1, ldo, epi, nullptr, 0, s);
+}
+
 bool gemv_split_supported(int M, int N, int K, int S) {
   if (S < 1 || K % S) return false;
   return gemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32);
 }
 
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
-                       int force_waves, hipStream_t s) {
-  gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, nullptr, force_waves, s);
+                       int force_waves, hipStream_t s, const GemvArgs* ga) {
+  gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, ga, force_waves, s);
 }
 
 // ---------------------------------------------------------------- argmax of partials

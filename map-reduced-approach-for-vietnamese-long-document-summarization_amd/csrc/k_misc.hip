@@ -12,12 +12,16 @@ thread_local ProfEvents* g_prof = nullptr;
 
 // ---------------------------------------------------------------- embedding
 // x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores
+// ssq (optional): ssq[t] = sum of x[t][:]^2 (fixed order: per thread, then the wave tree, then
+// the 4 waves in order) -- the one-tile RMSNorm statistics a kXNorm GEMV prologue consumes
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
                                                     const bf16_t* __restrict__ emb, int H,
-                                                    float* __restrict__ x) {
+                                                    float* __restrict__ x, float* __restrict__ ssq) {
+  __shared__ float red[4];
   const int t = blockIdx.x;
   const bf16_t* row = emb + (size_t)ids[t] * H;
   float* xo = x + (size_t)t * H;
+  float ss = 0.f;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     uint4 v = *(const uint4*)(row + c * 8);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -28,7 +32,13 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
     b.z = __uint_as_float(w[3] << 16); b.w = __uint_as_float(w[3] & 0xFFFF0000u);
     *(float4*)(xo + c * 8) = a;
     *(float4*)(xo + c * 8 + 4) = b;
+    ss += ((a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w)) + ((b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w));
   }
+  if (!ssq) return;  // block-uniform
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssq[t] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 // Chained decode steps (engine.cpp decode_run): the step's argmax ids become the next
@@ -59,9 +69,10 @@ void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring,
   MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
 }
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
+                  float* ssq) {
   if (T <= 0) return;
-  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
+  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x, ssq);
 }
 
 // ---------------------------------------------------------------- RMSNorm

@@ -34,7 +34,9 @@ struct DecodeAttnArgs {
   int32_t ppw;              // pages per wave, fixed per engine (attn_decode_ppw); 0 = 2
 };
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
+// ssq: optional per-row sums of squares [T] (one RMSNorm-statistics tile, see gemv_norm_x)
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
+                  float* ssq = nullptr);
 // chained decode: next ids <- this step's argmax (clamped into [0, V)), positions and key
 // counts += 1 in the step-argument blob [ids | positions | slots | key counts | step], and the
 // raw ids appended to ring row `step` (B <= 256)
@@ -64,7 +66,11 @@ enum {
   MS_GEMV_EPI_ROPE_KV = 4,
   // greedy argmax partials: out = {max, id} float2 [M][tiles] of each 16-column tile
   // (ties -> lowest id, NaN never wins); launch_argmax_partials finishes the rows
-  MS_GEMV_EPI_ARGMAX = 5
+  MS_GEMV_EPI_ARGMAX = 5,
+  // residual update + RMSNorm statistics (decode O / down, no split-K): out = x fp32 [M][ldo],
+  // x[r][c] += acc, and ga.ssq_out[tile][r] = sum over the tile's columns of the new x[r][c]^2
+  // (a fixed lane tree): the next GEMV's kXNorm prologue finishes the RMSNorm from them
+  MS_GEMV_EPI_RESID_SSQ = 6
 };
 struct GemvArgs {
   // ROPE_KV epilogue: Q -> out[row][h*128..] (ld = ldo), K/V -> paged cache
@@ -74,12 +80,30 @@ struct GemvArgs {
   const float* sin_tab;
   KVView kv;
   int Hq, Hk;
+  // weight rows per tile (NT = 1 plans; 0 = 16): 12 puts the 3072-row O / down projections on
+  // exactly 256 workgroups (one per CU) without split-K
+  int rt;
+  // RESID_SSQ epilogue: per-tile sums of squares [tiles][M]
+  float* ssq_out;
+  // RMSNorm prologue (X = bf16(rmsnorm(xres) * gamma) built in LDS, no separate norm launch):
+  // xres fp32 [M][hdim], ssq_in [ssq_tiles][M] from the RESID_SSQ producer, gamma bf16 [hdim]
+  const float* xres;
+  const float* ssq_in;
+  const bf16_t* gamma;
+  int ssq_tiles, hdim;
+  float eps;
 };
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm)
 bool gemv_split_supported(int M, int N, int K, int S);
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
-                       int force_waves, hipStream_t s);
+                       int force_waves, hipStream_t s, const GemvArgs* ga = nullptr);
+// whether a GEMV (plain or one split of a split-K launch, K = its slice) can build its X as
+// the RMSNorm of the fp32 residual itself (GemvArgs.xres/ssq_in/gamma: the kXNorm prologue)
+bool gemv_norm_supported(int M, int N, int K, int epi, int ssq_tiles, int rt);
+// X [M][ldk] and W [N][ldk] rows of stride ldk >= K (tuning hook: padded weight layouts)
+void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                         int ldo, int epi, hipStream_t s);
 // rows of {max, id} partials [rows][tiles] -> ids (-1: no finite maximum)
 void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* out, hipStream_t s);
 

@@ -33,6 +33,7 @@ EXPORTED = (
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_dgemm", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
+    "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
 )
 
 
@@ -59,7 +60,7 @@ class MsStats(C.Structure):
                 ("prefill_passes", C.c_int64), ("decode_steps", C.c_int64), ("finished", C.c_int64),
                 ("prefill_ms", C.c_double), ("decode_ms", C.c_double),
                 ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8),
-                ("decode_kv_tokens", C.c_int64)]
+                ("decode_kv_tokens", C.c_int64), ("graphs_built", C.c_int64)]
 
 
 _lib = None
@@ -97,6 +98,10 @@ def load() -> C.CDLL:
         "ms_set_profiling": (i32, [vp, u32]),
         "ms_synchronize": (i32, [vp]),
         "ms_forward": (i32, [vp, pi32, i32, i32, vp, vp]),
+        "ms_forward_packed": (i32, [vp, pi32, pi32, i32, i32, vp, vp]),
+        "ms_set_eos_ids": (i32, [vp, pi32, i32]),
+        "ms_op_gemv_strided": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "ms_submit_forced": (i32, [vp, pi32, i32, pi32, i32, i32, u32, u64]),
         "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_workspace": (i64, [i32, i32, i32]),
         "ms_op_gemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, vp]),

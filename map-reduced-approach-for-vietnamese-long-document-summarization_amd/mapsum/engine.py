@@ -171,6 +171,12 @@ class Engine(RequestQueue):
         a = np.ascontiguousarray(bf16_bits, dtype=np.uint16)
         self._chk(self.lib.ms_load_weight(self.h, tensor, layer, a.ctypes.data, a.size), "ms_load_weight")
 
+    def set_eos_ids(self, ids):
+        """Replace the end-of-turn ids by a stop set (empty: back to the config's)."""
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        self._chk(self.lib.ms_set_eos_ids(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)) if a.size else None,
+                                          a.size), "ms_set_eos_ids")
+
     # ------------------------------------------------------------ request path
     def submit(self, ids, num_predict: int, ignore_eos: bool = False, tag: int | None = None) -> int:
         a = np.ascontiguousarray(ids, dtype=np.int32)
@@ -181,6 +187,36 @@ class Engine(RequestQueue):
         self._chk(self.lib.ms_submit(self.h, a.ctypes.data_as(C.POINTER(C.c_int32)), a.size,
                                      int(num_predict), flags, int(tag)), "ms_submit")
         return tag
+
+    def submit_forced(self, ids, forced, num_predict: int, ignore_eos: bool = True) -> int:
+        """Teacher forcing through the decode path (parity tests): decode step j is fed
+        ``forced[j-1]``; the result ids are the engine's own greedy choices."""
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        f = np.ascontiguousarray(forced, dtype=np.int32)
+        if f.size == 0:
+            f = np.zeros(1, np.int32)
+        tag = self._next_tag
+        self._next_tag += 1
+        flags = L.MS_FLAG_IGNORE_EOS if ignore_eos else 0
+        p32 = C.POINTER(C.c_int32)
+        self._chk(self.lib.ms_submit_forced(self.h, a.ctypes.data_as(p32), a.size, f.ctypes.data_as(p32),
+                                            f.size, int(num_predict), flags, int(tag)), "ms_submit_forced")
+        return tag
+
+    def generate_forced(self, prompts, forced, num_predict: int) -> list:
+        """ids[j] = the engine's greedy choice at step j after prompt + forced[:j]."""
+        tags = [self.submit_forced(p, f, num_predict) for p, f in zip(prompts, forced)]
+        waiting = set(tags)
+        got = {}
+        while waiting:
+            pending = self.step()
+            self.collect()
+            for t, r in self.take(waiting).items():
+                waiting.discard(t)
+                got[t] = r
+            if pending == 0 and waiting and not any(t in self._mailbox for t in waiting):
+                raise RuntimeError("engine drained without finishing every request")
+        return [got[t] for t in tags]
 
     def step(self) -> int:
         return self._chk(self.lib.ms_step(self.h), "ms_step")
@@ -211,6 +247,21 @@ class Engine(RequestQueue):
                                       lg.ctypes.data if lg is not None else None), "ms_forward")
         return hid, lg
 
+    def forward_packed(self, prompts, n_layers: int | None = None, hidden: bool = True, logits: bool = False):
+        """ms_forward_packed: the prompts in ONE varlen prefill pass; rows in packed order."""
+        cfg = self.cfg
+        a = np.ascontiguousarray(np.concatenate([np.asarray(p, np.int32) for p in prompts]), dtype=np.int32)
+        lens = np.ascontiguousarray([len(p) for p in prompts], dtype=np.int32)
+        n = a.size
+        nl = cfg.n_layers if n_layers is None else n_layers
+        hid = np.empty((n, cfg.hidden), np.float32) if hidden else None
+        lg = np.empty((n, cfg.vocab), np.float32) if logits else None
+        p32 = C.POINTER(C.c_int32)
+        self._chk(self.lib.ms_forward_packed(self.h, a.ctypes.data_as(p32), lens.ctypes.data_as(p32), lens.size,
+                                             nl, hid.ctypes.data if hid is not None else None,
+                                             lg.ctypes.data if lg is not None else None), "ms_forward_packed")
+        return hid, lg
+
     def set_profiling(self, mask: int):
         self._chk(self.lib.ms_set_profiling(self.h, mask), "ms_set_profiling")
 
@@ -227,4 +278,4 @@ class Engine(RequestQueue):
                 "prefill_passes": s.prefill_passes, "decode_steps": s.decode_steps,
                 "finished": s.finished, "prefill_ms": s.prefill_ms, "decode_ms": s.decode_ms,
                 "kernel_ms": list(s.kernel_ms), "kernel_launches": list(s.kernel_launches),
-                "decode_kv_tokens": s.decode_kv_tokens}
+                "decode_kv_tokens": s.decode_kv_tokens, "graphs_built": s.graphs_built}

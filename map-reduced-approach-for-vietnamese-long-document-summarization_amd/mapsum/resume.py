@@ -44,13 +44,22 @@ class CallJournal:
         self._done: dict = {}
         self.torn_lines = 0
         if os.path.exists(path):
-            with open(path, "r", encoding="utf-8") as f:
-                for line in f:
-                    try:
-                        rec = json.loads(line)
-                        self._done[rec["k"]] = rec["text"]
-                    except (json.JSONDecodeError, KeyError, TypeError):
-                        self.torn_lines += 1  # a crash mid-write: that call is simply re-run
+            # a crash mid-write leaves a torn last line with no newline: cut the file back to
+            # the last complete record so the next put() starts on a fresh line (appending onto
+            # the fragment would tear that record too); the torn call is simply re-run
+            with open(path, "rb+") as f:
+                data = f.read()
+                keep = data.rfind(b"\n") + 1
+                if keep < len(data):
+                    f.truncate(keep)
+                    self.torn_lines += 1
+                    data = data[:keep]
+            for line in data.decode("utf-8", errors="replace").splitlines():
+                try:
+                    rec = json.loads(line)
+                    self._done[rec["k"]] = rec["text"]
+                except (json.JSONDecodeError, KeyError, TypeError):
+                    self.torn_lines += 1
         d = os.path.dirname(os.path.abspath(path))
         os.makedirs(d, exist_ok=True)
         self._f = open(path, "a", encoding="utf-8")

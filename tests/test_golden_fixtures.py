@@ -1,0 +1,58 @@
+"""The committed 28-layer fixtures (tests/golden/make_fullshape_golden.py) are what they claim
+to be -- CPU only; the GPU comparison is tests/test_gpu_golden28.py."""
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+sys.path.insert(0, GOLD)
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(os.path.dirname(HERE), "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    return b
+
+
+@pytest.mark.parametrize("which", ["flat", "sharp"])
+def test_fixture_layout_and_prompts(which):
+    from mapsum.config import LLAMA32_3B as C
+    d = np.load(os.path.join(GOLD, f"fullshape_{which}.npz"))
+    meta = json.loads(bytes(d["meta"]).decode())
+    assert meta["which"] == which and meta["n_layers"] == C.n_layers == 28 and meta["prompt_len"] == 2048
+    chunks = _bench().synthetic_chunks(8, 2048, doc=0, vocab=C.vocab, bos=C.bos_id)
+    for ci in meta["chunks"]:
+        k = f"c{ci}_"
+        assert np.array_equal(d[k + "prompt"], chunks[ci])  # configs[1]'s own chunks
+        assert d[k + "hid_rows"].shape == (28, 3, C.hidden) and d[k + "hid_norm"].shape == (28, 2048)
+        assert d[k + "hid_sketch"].shape == (28, 512, 8)
+        assert d[k + "gen_ids"].shape == (meta["gen"],) and meta["gen"] >= 128
+        tv = d[k + "gen_top_vals"]
+        assert np.all(np.diff(tv, axis=1) <= 0)  # top-16 sorted
+        assert np.array_equal(d[k + "gen_ids"], d[k + "gen_top_ids"][:, 0])  # greedy = top-1
+        # the residual grows through the stack (the sketch is not all zeros / NaN)
+        assert np.all(np.isfinite(d[k + "hid_norm"])) and np.all(d[k + "hid_norm"][-1] > 0)
+
+
+def test_sharp_fixture_is_decisive_and_copies():
+    """The sharp model's oracle continuation is the copy head's (token(p+1) = token(p-36)) with
+    top-2 gaps far above any bf16 logit noise; the flat one has near-ties (why it exists)."""
+    import sharp_model
+    d = np.load(os.path.join(GOLD, "fullshape_sharp.npz"))
+    meta = json.loads(bytes(d["meta"]).decode())
+    assert meta["copy_offset"] == sharp_model.COPY_OFFSET
+    for ci in meta["chunks"]:
+        k = f"c{ci}_"
+        n = len(d[k + "gen_ids"])
+        assert list(d[k + "gen_ids"]) == sharp_model.expected_continuation(d[k + "prompt"], n)
+        gap = d[k + "gen_top_vals"][:, 0] - d[k + "gen_top_vals"][:, 1]
+        assert gap.min() > 10.0
+    f = np.load(os.path.join(GOLD, "fullshape_flat.npz"))
+    gap = f["c0_gen_top_vals"][:, 0] - f["c0_gen_top_vals"][:, 1]
+    assert gap.min() < 0.01  # flat logits: near-ties exist

@@ -349,3 +349,77 @@ def test_fullshape_q4_k_m_engine_vs_oracle(dev):
         assert np.mean(want[dec] == gen[dec]) >= 0.99
     finally:
         e.close()
+
+
+# ------------------------------------------------- configs[2] and configs[3] at full width
+def _tf_check(oracle, prompt, gen, tag):
+    """Teacher-forced oracle logits after the engine's own tokens; every disagreement must be
+    an oracle near-tie.  Returns the agreement fraction."""
+    cache = oracle.new_cache()
+    first, _ = oracle.forward(prompt, cache)
+    lg = _teacher_forced(oracle, cache, first, gen)
+    want = np.argmax(lg, 1)
+    srt = np.sort(lg, 1)
+    for j in np.nonzero(want != gen)[0]:
+        assert srt[j, -1] - lg[j, gen[j]] <= 1e-2 * (abs(srt[j, -1]) + 1.0), (tag, j)
+    return float(np.mean(want == gen))
+
+
+@pytest.mark.timeout(1200)
+def test_config2_continuous_batching_full_width(oracle):
+    """BASELINE configs[2] per GPU at full width (2 layers): max_batch 128 slots over 2304-token
+    contexts, 160 chunks of 2048 tokens (more chunks than slots: admission as slots free),
+    32 greedy tokens each.  The B=128 decode plan (skinny GEMM regime, per-engine attention
+    pages-per-wave) against the oracle for three chunks, and batch invariance against solo
+    runs (runners/run_summarization_ollama_mapreduce.py:109-112 hands the engine every chunk)."""
+    import importlib.util
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    chunks = [c for d in range(20) for c in bench.synthetic_chunks(8, P, doc=d, vocab=CFG.vocab, bos=CFG.bos_id)]
+    e = Engine(CFG, device=0, max_batch=128, max_ctx=P + 256, max_prefill_tokens=8 * P)
+    try:
+        e.init_synthetic(SEED, STD, JIT)
+        res = e.generate(chunks, num_predict=32, ignore_eos=True)
+        assert all(len(r.ids) == 32 and r.finish == "length" for r in res)
+        for i in (0, 77, 159):
+            agree = _tf_check(oracle, chunks[i], np.asarray(res[i].ids), i)
+            print(f"configs[2] chunk {i}: teacher-forced agreement {agree:.4f}")
+        for i in (5, 130):
+            alone = e.generate([chunks[i]], num_predict=32, ignore_eos=True)[0]
+            assert alone.ids == res[i].ids, i
+    finally:
+        e.close()
+
+
+@pytest.mark.timeout(1200)
+def test_config3_ragged_sections_full_width(oracle):
+    """BASELINE configs[3] at full width (2 layers): ragged hierarchical sections of 64, 611,
+    1500 and 4096 tokens packed into ONE varlen prefill pass (max_ctx 4352): per-layer hidden
+    states of every section against the oracle, then 64 greedy tokens per section in one
+    continuous batch, teacher-forced against the oracle
+    (runners/run_summarization_ollama_mapreduce_hierarchical.py:242-274)."""
+    rng = np.random.default_rng(11)
+    lens = (64, 611, 1500, 4096)
+    secs = [rng.integers(0, 128000, size=n).astype(np.int32) for n in lens]
+    e = Engine(CFG, device=0, max_batch=4, max_ctx=4352, max_prefill_tokens=8192)
+    try:
+        e.init_synthetic(SEED, STD, JIT)
+        offs = np.cumsum((0,) + lens)
+        probes = [oracle.forward(s, collect=True)[1] for s in secs]
+        for l in range(CFG.n_layers):
+            h, _ = e.forward_packed(secs, n_layers=l + 1)
+            for i, s in enumerate(secs):
+                err = rel(h[offs[i]:offs[i + 1]], probes[i][l])
+                print(f"configs[3] layer {l} section {len(s)}: hidden rel err {err:.3e}")
+                assert err < 2e-2, (l, len(s))
+        del probes
+        res = e.generate(secs, num_predict=64, ignore_eos=True)
+        for s, r in zip(secs, res):
+            assert len(r.ids) == 64
+            agree = _tf_check(oracle, s, np.asarray(r.ids), len(s))
+            print(f"configs[3] section {len(s)}: teacher-forced agreement {agree:.4f}")
+    finally:
+        e.close()

@@ -58,6 +58,11 @@ def test_journal_roundtrip_and_torn_line(tmp_path):
     j = CallJournal(str(p))
     assert len(j) == 2 and j.get("k1") == "một" and j.get("k2") == "hai"
     assert j.torn_lines == 1 and "k3" not in j
+    # a write after the torn line must survive the next reload (the fragment was cut away)
+    j.put("k4", "d", "bốn")
+    j.close()
+    j = CallJournal(str(p))
+    assert len(j) == 3 and j.get("k4") == "bốn" and j.torn_lines == 0
     j.close()
 
 

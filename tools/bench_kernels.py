@@ -189,6 +189,34 @@ def bench_qgemv(lib, M):
         print(line, flush=True)
 
 
+def bench_camp(lib, M):
+    """Unsplit decode GEMV over weight rows padded to ldk = K + pad elements: does the row
+    stride (16 KB for the down projection) concentrate a launch on a few HBM channels?"""
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, N, K, epi in [("o", 3072, 3072, 1), ("down", 3072, 8192, 1), ("qkv", 5120, 3072, 3),
+                            ("gu-like", 16384, 3072, 3)]:
+        line = f"{name:8s} N={N:6d} K={K:5d} M={M:2d} |"
+        for pad in (0, 64, 128, 256, 512):
+            ldk = K + pad
+            Ws = [torch.randn(N, ldk, device=dev).to(torch.bfloat16) * 0.02
+                  for _ in range(max(2, -(-512 * 2**20 // (N * ldk * 2))))]
+            X = torch.randn(M, ldk, device=dev).to(torch.bfloat16)
+            out = torch.zeros(M, N, device=dev)
+            i = [0]
+
+            def fn():
+                i[0] += 1
+                rc = lib.ms_op_gemv_strided(X.data_ptr(), Ws[i[0] % len(Ws)].data_ptr(), out.data_ptr(), M, N, K,
+                                            ldk, N, epi, st)
+                if rc:
+                    raise RuntimeError(lib.ms_last_error(None))
+            t = timeit(fn)
+            line += f" pad{pad}: {t*1e3:6.1f}us {N*K*2/t/1e6:5.0f} |"
+            del Ws
+        print(line, flush=True)
+
+
 def bench_gemm(lib):
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
@@ -213,7 +241,7 @@ def bench_gemm(lib):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp"])
     ap.add_argument("--m", type=int, default=8)
     a = ap.parse_args()
     lib = L.load()
@@ -227,5 +255,7 @@ if __name__ == "__main__":
         bench_dgemm(lib)
     elif a.what == "qgemv":
         bench_qgemv(lib, a.m)
+    elif a.what == "camp":
+        bench_camp(lib, a.m)
     else:
         bench_gemm(lib)
