@@ -128,12 +128,16 @@ struct ms_engine {
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
-  // norm-fused decode (engines of <= kNormMaxBatch slots, bf16 weights; MS_NORM_FUSED=0 turns it
-  // off): no residual_rmsnorm launches -- O and down run unsplit on norm_rt-row tiles (3072 / 12
+  // norm-fused decode (engines of <= kNormMaxBatch slots, bf16 weights; MS_NORM_FUSED=1): no
+  // residual_rmsnorm launches -- O and down run unsplit on norm_rt-row tiles (3072 / 12
   // = 256 workgroups) and add into the fp32 residual themselves, writing per-tile sums of squares
   // (ssq [tiles][B]); QKV and gate/up build their X as bf16(rmsnorm(x) * g) in their own
   // prologue from those sums (k_gemv.hip kXNorm).  Chosen per engine, like the regimes above.
-  bool norm_fuse = true, has_quant = false;
+  // Measured on MI355X at B = 8: 2.57 vs 2.25 ms per decode step -- every one of the hundreds
+  // of QKV / gate-up blocks loads x and the statistics before its weight stream starts (+10 /
+  // +7.5 us per launch against the 2 x 4.9 us norm launches it removes), so it stays off
+  // (profiles/r03/v1_norm_fused_ab.txt).
+  bool norm_fuse = false, has_quant = false;  // MS_NORM_FUSED=1: measured slower, see below
   int norm_rt = 12, ssq_tiles = 0;
   float* ssq = nullptr;
   static constexpr int kNormMaxBatch = 10;

@@ -40,10 +40,25 @@ __device__ __forceinline__ bf16x8 load_vt(const char* vs, int dt, int ks, int la
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1
+// B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1.  P enters the
+// P.V MFMAs as TWO bf16 operands, hi = bf16(p) and lo = bf16(p - hi), one MFMA each on the
+// same V^T fragment: p = hi + lo to ~16 bits, so P.V is fp32-accurate.  With hi alone the
+// rounding of P (2^-9 relative) made the attention output differ from the exact-softmax
+// arithmetic by ~1e-3, which the bf16 rounding of the output doubled and 28 layers compounded
+// to ~2e-2 in the final logits (tests/test_gpu_golden28.py; the Ollama CPU path rounds P to
+// fp16, 2^-11).
 __device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
   u4 v = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ bf16x8 pack_p_lo(const f32x4& a, const f32x4& b, bf16x8 hi) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4 h = __builtin_bit_cast(u4, hi);
+  auto lo16 = [](uint32_t w) { return __uint_as_float(w << 16); };
+  auto hi16 = [](uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); };
+  u4 v = {pack2bf(a[0] - lo16(h[0]), a[1] - hi16(h[0])), pack2bf(a[2] - lo16(h[1]), a[3] - hi16(h[1])),
+          pack2bf(b[0] - lo16(h[2]), b[1] - hi16(h[2])), pack2bf(b[2] - lo16(h[3]), b[3] - hi16(h[3]))};
   return __builtin_bit_cast(bf16x8, v);
 }
 
@@ -175,7 +190,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
             for (int hh = 0; hh < GB; ++hh) sc[hh][mt][j] = -INFINITY;
         }
     }
-    bf16x8 pf[GB][2];
+    bf16x8 pf[GB][2], pl[GB][2];
     bool rescale = false;
     float alpha[GB];
 #pragma unroll
@@ -212,6 +227,8 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       m_run[hh] = m_use;
       pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
+      pl[hh][0] = pack_p_lo(sc[hh][0], sc[hh][1], pf[hh][0]);
+      pl[hh][1] = pack_p_lo(sc[hh][2], sc[hh][3], pf[hh][1]);
     }
     if (__ballot(rescale) != 0) {
 #pragma unroll
@@ -225,7 +242,10 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       for (int dt = 0; dt < 8; ++dt) {
         const bf16x8 vt = load_vt(vs_, dt, kstep, lane);
 #pragma unroll
-        for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
+        for (int hh = 0; hh < GB; ++hh) {
+          o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
+          o[hh][dt] = mfma16(vt, pl[hh][kstep], o[hh][dt]);
+        }
       }
   }
   if (qi < qlen) {
@@ -524,8 +544,13 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
       for (int kstep = 0; kstep < 2; ++kstep) {
         const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
+        const bf16x8 pl = pack_p_lo(sc[2 * kstep], sc[2 * kstep + 1], pf);
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[dt] = mfma16(load_vt(vs_, dt, kstep, lane), pf, o[dt]);
+        for (int dt = 0; dt < 8; ++dt) {
+          const bf16x8 vt = load_vt(vs_, dt, kstep, lane);
+          o[dt] = mfma16(vt, pf, o[dt]);
+          o[dt] = mfma16(vt, pl, o[dt]);
+        }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
       __builtin_amdgcn_wave_barrier();

@@ -260,7 +260,7 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
     if (!gemv_norm_supported(M, N, K, epi, ga_in->ssq_tiles, rt)) return;  // callers check
     xm = kXNorm;
   }
-  const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds);
+  const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds || xm == kXNorm);
   if (lds > kMaxLds) return;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;

@@ -89,22 +89,24 @@ class RecursiveCharacterTextSplitter:
         return t or None
 
     def _merge(self, splits: list, sep: str) -> list:
+        # the current window is splits[lo:hi] (LangChain keeps it as a list it pops from the
+        # front; an index pair gives the same windows without the quadratic copies)
         sep_len = self.length(sep)
-        docs, cur, total = [], [], 0
+        docs, lo, hi, total = [], 0, 0, 0
         for d in splits:
             n = self.length(d)
-            if total + n + (sep_len if cur else 0) > self.chunk_size:
-                if cur:
-                    doc = self._join(cur, sep)
+            if total + n + (sep_len if hi > lo else 0) > self.chunk_size:
+                if hi > lo:
+                    doc = self._join(splits[lo:hi], sep)
                     if doc is not None:
                         docs.append(doc)
                     while total > self.chunk_overlap or (
-                            total + n + (sep_len if cur else 0) > self.chunk_size and total > 0):
-                        total -= self.length(cur[0]) + (sep_len if len(cur) > 1 else 0)
-                        cur = cur[1:]
-            cur.append(d)
-            total += n + (sep_len if len(cur) > 1 else 0)
-        doc = self._join(cur, sep)
+                            total + n + (sep_len if hi > lo else 0) > self.chunk_size and total > 0):
+                        total -= self.length(splits[lo]) + (sep_len if hi - lo > 1 else 0)
+                        lo += 1
+            hi += 1
+            total += n + (sep_len if hi - lo > 1 else 0)
+        doc = self._join(splits[lo:hi], sep)
         if doc is not None:
             docs.append(doc)
         return docs
