@@ -116,9 +116,10 @@ def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=16):
     from oracle.torch_cpu import time_chunk
     r = time_chunk(cfg, prompt_ids, gen_len, decode_sample=decode_sample)
     return {"value": round(1.0 / r["chunk_s"], 5), "unit": "chunks/s", "cores": int(r["threads"]),
-            "kind": "port",
-            "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16, "
-                       f"{cfg.n_layers}-layer Llama-3.2-3B, 1 chunk: {len(prompt_ids)}-tok prefill "
+            "kind": "port", "cpu_model": r["cpu_model"],
+            "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16 on {r['cpu_model']}, "
+                       f"{cfg.n_layers}-layer Llama-3.2-3B on the engine's own synthetic weights, "
+                       f"1 chunk: {len(prompt_ids)}-tok prefill "
                        f"{r['prefill_s']:.2f} s + {r['decode_steps_timed']} decode steps at "
                        f"{r['decode_step_s'] * 1e3:.1f} ms, extrapolated to {gen_len} tokens "
                        f"({r['chunk_s']:.1f} s/chunk)")}

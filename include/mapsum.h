@@ -216,6 +216,12 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
 /* tuning hook: ms_op_gemv over X [M][ldk] and W [N][ldk] (row stride ldk >= K elements) */
 int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                        int32_t ldk, int32_t ldo, int32_t epilogue, void* stream);
+/* persistent decode GEMV (one block per CU walking its 16-row tiles with the next tile's weights
+   in flight): epilogue MS_EPI_STORE_F32 into split-K slabs [S][M][N] (ldo = N), or MS_EPI_SWIGLU
+   with S = 1 (out bf16 [M][ldo = N/2]); M <= 16, (K/S) % 64 == 0.  Same sums as ms_op_gemv_split
+   (S slices) / ms_op_gemv (SwiGLU), bit for bit. */
+int ms_op_pgemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
+                int32_t ldo, int32_t epilogue, void* stream);
 /* large-batch decode GEMM (M <= 256 rows; 64 weight rows per block, X shared via LDS): the
    ms_op_gemv epilogues (plus MS_EPI_ARGMAX); S > 1: split-K fp32 slabs [S][M][N] with
    epilogue MS_EPI_STORE_F32; N % 64 == 0, K % (64 S) == 0 */

@@ -149,6 +149,15 @@ struct ms_engine {
   // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the bf16 splits (6 / 6 / 4), 2 / 3 / 8
   // slower (profiles/r02/v27_qsplit_sweep_q4_k_m.txt)
   int qsplit = 4;
+  // persistent decode GEMVs (k_gemv.hip pgemv_kernel: one block per CU walking its tiles) for
+  // the bf16 projections of small-regime engines: QKV / O / down as psplit-way split-K slabs
+  // (4: 5 / 3 / 3 tiles per block, evenly balanced over 256 CUs), gate/up + SwiGLU unsplit.
+  // Measured on MI355X at B = 8 (profiles/r03/v2_pgemv_ab.txt): slower on every projection
+  // (gate/up 21.1 vs 19.4 us, QKV / O 7.9 vs 7.0, down 12.9 vs 12.6; 2.357 vs 2.255 ms per
+  // decode step) -- one block per CU with two register stages keeps fewer bytes in flight than
+  // two co-resident one-tile blocks -- so one block per tile stays the default (MS_PGEMV=1: A/B).
+  bool use_pgemv = false;
+  int psplit = 4;
   // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
   // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
   bool attn_slabs = true, attn_fused_combine = false;
@@ -294,6 +303,9 @@ struct ms_engine {
       } else {
         launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
       }
+    } else if (use_pgemv && pgemv_supported(M, N, K, psplit, MS_GEMV_EPI_STORE_F32, false)) {
+      launch_pgemv(X, W, slabs, M, N, K, psplit, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
+      used = psplit;
     } else {
       if (!(S >= 1 && S <= kMaxSplit && gemv_split_supported(M, N, K, S))) S = 1;
       launch_gemv_split(X, W, slabs, M, N, K, S, 0, stream);
@@ -328,10 +340,16 @@ struct ms_engine {
     KVView kv = kv_layer(l);
     // QKV -> split-K slabs; each block normalises its slice of x with attn_norm first
     GemvArgs gq = norm_args(Ly.attn_norm);
+    int sq = split_qkv;
     prof_begin(K_GEMV);
-    launch_gemv_split(xb, Ly.wqkv, slabs, B, QKVN, H, split_qkv, 0, stream, &gq);
+    if (use_pgemv && pgemv_supported(B, QKVN, H, psplit, MS_GEMV_EPI_STORE_F32, true)) {
+      launch_pgemv(xb, Ly.wqkv, slabs, B, QKVN, H, psplit, QKVN, MS_GEMV_EPI_STORE_F32, &gq, stream);
+      sq = psplit;
+    } else {
+      launch_gemv_split(xb, Ly.wqkv, slabs, B, QKVN, H, split_qkv, 0, stream, &gq);
+    }
     prof_end(K_GEMV);
-    DecodeQKV qa{nullptr, slabs, split_qkv, cos_tab, sin_tab};
+    DecodeQKV qa{nullptr, slabs, sq, cos_tab, sin_tab};
     prof_begin(K_ATTN_DECODE);
     launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
     prof_end(K_ATTN_DECODE);
@@ -345,7 +363,10 @@ struct ms_engine {
     ssq_tiles = (H + norm_rt - 1) / norm_rt;
     GemvArgs gg = norm_args(Ly.ffn_norm);
     prof_begin(K_GEMV);
-    launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, 0, stream);
+    if (use_pgemv && pgemv_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU, true))
+      launch_pgemv(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, &gg, stream);
+    else
+      launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, 0, stream);
     prof_end(K_GEMV);
     prof_begin(K_GEMV);
     launch_gemv_ex(hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_RESID_SSQ, &go, 0, stream);
@@ -389,6 +410,10 @@ struct ms_engine {
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
       prof_begin(K_GEMV);
       launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream);
+      prof_end(K_GEMV);
+    } else if (use_pgemv && !Q[QS_GU].ready() && pgemv_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU, false)) {
+      prof_begin(K_GEMV);
+      launch_pgemv(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, nullptr, stream);
       prof_end(K_GEMV);
     } else {
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
@@ -640,6 +665,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     if (const char* v = getenv("MS_NORM_FUSED")) E.norm_fuse = atoi(v) != 0;
+    if (const char* v = getenv("MS_PGEMV")) E.use_pgemv = atoi(v) != 0;
+    if (cfg->max_batch > 16) E.use_pgemv = false;  // per engine: every step the same arithmetic
+    if (const char* v = getenv("MS_PSPLIT")) E.psplit = std::max(1, atoi(v));
     if (E.H % E.norm_rt || E.H / E.norm_rt > 256) E.norm_rt = 16;
     E.norm_fuse = E.norm_fuse && E.H % E.norm_rt == 0 && E.H / E.norm_rt <= 256 &&
                   gemv_norm_supported(cfg->max_batch, E.QKVN, E.H / E.split_qkv, MS_GEMV_EPI_STORE_F32,
@@ -1508,6 +1536,16 @@ int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32
     REQUIRE(epi >= 0 && epi <= 3 && epi != MS_EPI_SWIGLU, MS_EINVAL, "bad epilogue");
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported");
     launch_gemv_strided((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldk, ldo, epi, (hipStream_t)stream);
+  });
+}
+
+int ms_op_pgemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
+                int32_t ldo, int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && W && out, MS_EINVAL, "bad pgemv operands");
+    REQUIRE(pgemv_supported(M, N, K, S, epi, false), MS_EINVAL,
+            "pgemv shape unsupported (M <= 16; STORE_F32 slabs or SWIGLU with S = 1; (K/S) % 64 == 0)");
+    launch_pgemv((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, nullptr, (hipStream_t)stream);
   });
 }
 

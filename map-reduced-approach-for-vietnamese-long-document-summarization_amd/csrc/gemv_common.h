@@ -143,12 +143,15 @@ __device__ __forceinline__ void amax_merge_dev(float& v, int& i, float v2, int i
 // Cross-wave reduction of the per-wave MFMA accumulators through LDS and the epilogue.
 // acc[m][n][j] = C[row m*16 + 4*(lane>>4) + j][col n0 + n*16 + (lane&15)].
 template <int MT, int NT, int EPI>
+__device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, int ldo,
+                                              void* __restrict__ out, int n0, const GemvArgs& ga);
+
+template <int MT, int NT, int EPI>
 __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, int M, int N,
                                             int ldo, void* __restrict__ out, int n0,
                                             const GemvArgs& ga) {
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nthreads = blockDim.x, nw = nthreads >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __syncthreads();  // X image no longer needed: reuse LDS for the partials
   float* red = (float*)smem;
 #pragma unroll
@@ -157,6 +160,16 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
     for (int n = 0; n < NT; ++n)
       *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
   __syncthreads();
+  gemv_epilogue<MT, NT, EPI>(red, M, N, ldo, out, n0, ga);
+}
+
+// The epilogue of a decode GEMV tile from the per-wave partials in LDS (red[wave][elem]).
+template <int MT, int NT, int EPI>
+__device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, int ldo,
+                                              void* __restrict__ out, int n0, const GemvArgs& ga) {
+  constexpr int ELEMS = MT * NT * 256;
+  const int tid = threadIdx.x;
+  const int nthreads = blockDim.x, nw = nthreads >> 6;
   // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
   auto sum_e = [&](int e) {
     float v = 0.f;

@@ -293,6 +293,157 @@ void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, in
   gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, ga, force_waves, s);
 }
 
+// ---------------------------------------------------------------- persistent decode GEMV
+// One block per CU for the whole launch.  Block b owns ONE K slice (split s = b % S, K = the
+// slice length) and walks the 16*NT-row tiles t = b / S, + G/S, ... of N: its X slice is
+// staged in LDS ONCE (DMA of the bf16 rows, or built as bf16(rmsnorm(x) * gamma) by the
+// kXNorm prologue), and while a tile is multiplied, reduced across the waves and written, the
+// next tile's weights are already in flight (two register stages).  Compared with one block
+// per tile (gemv_kernel), the per-block X staging, ramp and tail are paid once per CU instead
+// of once per tile, and a CU's weight stream never stops between its tiles.  Results are
+// identical to gemv_kernel's for the same (N, K, S): a tile's summation order is the same
+// (wave slices of U steps, LDS reduction in wave order).
+template <int NT, int EPI, int U, int XM>
+__global__ __launch_bounds__(1024) void pgemv_kernel(const bf16_t* __restrict__ X,
+                                                     const bf16_t* __restrict__ W,
+                                                     void* __restrict__ out, int M, int N, int K,
+                                                     int ldk, int ldo, int S, GemvArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ELEMS = NT * 256;  // floats of one wave's tile result
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int split = blockIdx.x % S, per = gridDim.x / S;
+  const int rows = 16 * NT, ntiles = (N + rows - 1) / rows;
+  const int kbeg = wave * U * 64;
+  float* red0 = (float*)(smem + gemv_x_lds_bytes(M, K) + 64);
+  float* red1 = red0 + nw * ELEMS;
+  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
+    X += (size_t)split * K;
+    W += (size_t)split * K;
+    out = (float*)out + (size_t)split * M * ldo;
+  }
+  if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
+  uint4 wa[U][NT][2], wb[U][NT][2];
+  auto load = [&](uint4 (&w)[U][NT][2], int t) {
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const bf16_t* wp = W + (size_t)min(t * rows + n * 16 + fr, N - 1) * ldk + kbeg + 16 * fg;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        w[u][n][0] = ldw16(wp + u * 64);
+        w[u][n][1] = ldw16(wp + u * 64 + 8);
+      }
+    }
+  };
+  auto tile = [&](const uint4 (&w)[U][NT][2], int t, float* red) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int xrow = min(fr, M - 1);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k0 = kbeg + u * 64 + 16 * fg;
+      const bf16x8 x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
+      const bf16x8 x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        acc[n] = mfma16(x0, as_bf16x8(w[u][n][0]), acc[n]);
+        acc[n] = mfma16(x1, as_bf16x8(w[u][n][1]), acc[n]);
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NT; ++n) *(f32x4*)&red[wave * ELEMS + (n * 64 + lane) * 4] = acc[n];
+    lds_sync();  // LDS only: the next tile's weights stay in flight
+    gemv_epilogue<1, NT, EPI>(red, M, N, ldo, out, t * rows, ga);
+  };
+  int t = blockIdx.x / S;
+  if (t < ntiles) load(wa, t);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (XM == kXNorm) gemv_norm_x(smem, ga, M, K, split * K);
+  if constexpr (XM == kXLds) {
+    // the X image landed once at most this block's first weight loads are pending
+    if (t < ntiles) __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    __builtin_amdgcn_s_barrier();
+  }
+  while (t < ntiles) {
+    const int t1 = t + per;
+    if (t1 < ntiles) load(wb, t1);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(wa, t, red0);
+    t = t1;
+    if (t >= ntiles) break;
+    const int t2 = t + per;
+    if (t2 < ntiles) load(wa, t2);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(wb, t, red1);
+    t = t2;
+  }
+}
+
+struct PgemvPlan {
+  int waves, U, grid;
+};
+// waves <= 16 splitting the slice's 64-wide steps evenly with U <= 4 (two register stages of
+// U*NT*2 uint4 per lane), grid = one block per CU rounded down to a multiple of S
+static PgemvPlan pgemv_plan(int N, int Ks, int S, int NT) {
+  PgemvPlan p{0, 0, 0};
+  const int steps = Ks / 64;
+  for (int w = 16; w >= 4; --w)
+    if (steps % w == 0 && steps / w <= 4 && (steps / w) * NT <= 6) { p.waves = w; p.U = steps / w; break; }
+  p.grid = (256 / S) * S;
+  return p;
+}
+
+static size_t pgemv_lds_bytes(const PgemvPlan& p, int M, int Ks, int NT) {
+  return gemv_x_lds_bytes(M, Ks) + 64 + 2 * (size_t)p.waves * NT * 256 * 4;
+}
+
+bool pgemv_supported(int M, int N, int K, int S, int epi, bool norm) {
+  if (M < 1 || M > 16 || S < 1 || K % S || (K / S) % 64) return false;
+  if (epi != MS_GEMV_EPI_STORE_F32 && epi != MS_GEMV_EPI_SWIGLU) return false;
+  if (S > 1 && epi != MS_GEMV_EPI_STORE_F32) return false;
+  const int NT = epi == MS_GEMV_EPI_SWIGLU ? 2 : 1;
+  if (N % (16 * NT)) return false;
+  const PgemvPlan p = pgemv_plan(N, K / S, S, NT);
+  if (p.waves == 0 || p.grid < S) return false;
+  (void)norm;
+  return pgemv_lds_bytes(p, M, K / S, NT) <= kMaxLds;
+}
+
+template <int NT, int EPI, int XM>
+static void pgemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int Ks, int ldk, int ldo,
+                     int S, const PgemvPlan& p, const GemvArgs& ga, hipStream_t s) {
+  const size_t lds = pgemv_lds_bytes(p, M, Ks, NT);
+#define PG(U_) MS_LAUNCH((pgemv_kernel<NT, EPI, U_, XM>), dim3(p.grid), dim3(64 * p.waves), lds, s, X, W, out, M, \
+                         N, Ks, ldk, ldo, S, ga)
+  switch (p.U) {
+    case 1: PG(1); break;
+    case 2: PG(2); break;
+    case 3: PG(3); break;
+    default: PG(4); break;
+  }
+#undef PG
+}
+
+void launch_pgemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+                  const GemvArgs* ga_in, hipStream_t s) {
+  if (!pgemv_supported(M, N, K, S, epi, ga_in && ga_in->xres)) return;  // callers check
+  const int NT = epi == MS_GEMV_EPI_SWIGLU ? 2 : 1;
+  const int Ks = K / S;
+  const PgemvPlan p = pgemv_plan(N, Ks, S, NT);
+  GemvArgs ga{};
+  if (ga_in) ga = *ga_in;
+  const bool norm = ga.xres != nullptr;
+  if (epi == MS_GEMV_EPI_SWIGLU) {
+    if (norm) pgemv_go<2, MS_GEMV_EPI_SWIGLU, kXNorm>(X, W, out, M, N, Ks, K, ldo, S, p, ga, s);
+    else pgemv_go<2, MS_GEMV_EPI_SWIGLU, kXLds>(X, W, out, M, N, Ks, K, ldo, S, p, ga, s);
+  } else {
+    if (norm) pgemv_go<1, MS_GEMV_EPI_STORE_F32, kXNorm>(X, W, out, M, N, Ks, K, N, S, p, ga, s);
+    else pgemv_go<1, MS_GEMV_EPI_STORE_F32, kXLds>(X, W, out, M, N, Ks, K, N, S, p, ga, s);
+  }
+}
+
 // ---------------------------------------------------------------- argmax of partials
 // rows of {max, id} float2 partials (MS_GEMV_EPI_ARGMAX) -> greedy ids; ties -> lowest id
 // whatever the merge order; -1 when the row has no finite maximum (a failed chunk)

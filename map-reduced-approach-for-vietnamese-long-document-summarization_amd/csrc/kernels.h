@@ -98,6 +98,11 @@ struct GemvArgs {
 bool gemv_split_supported(int M, int N, int K, int S);
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga = nullptr);
+// persistent decode GEMV (one block per CU walking its tiles, next tile's weights in flight):
+// STORE_F32 split-K slabs [S][M][N] (ldo = N) or SWIGLU (S = 1); ga->xres set = kXNorm prologue
+bool pgemv_supported(int M, int N, int K, int S, int epi, bool norm);
+void launch_pgemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+                  const GemvArgs* ga, hipStream_t s);
 // whether a GEMV (plain or one split of a split-K launch, K = its slice) can build its X as
 // the RMSNorm of the fp32 residual itself (GemvArgs.xres/ssq_in/gamma: the kXNorm prologue)
 bool gemv_norm_supported(int M, int N, int K, int epi, int ssq_tiles, int rt);

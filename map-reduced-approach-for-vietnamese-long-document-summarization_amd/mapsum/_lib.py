@@ -34,6 +34,7 @@ EXPORTED = (
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
+    "ms_op_pgemv",
 )
 
 
@@ -101,6 +102,7 @@ def load() -> C.CDLL:
         "ms_forward_packed": (i32, [vp, pi32, pi32, i32, i32, vp, vp]),
         "ms_set_eos_ids": (i32, [vp, pi32, i32]),
         "ms_op_gemv_strided": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "ms_op_pgemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
         "ms_submit_forced": (i32, [vp, pi32, i32, pi32, i32, i32, u32, u64]),
         "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_workspace": (i64, [i32, i32, i32]),

@@ -19,25 +19,73 @@ import time
 import torch
 import torch.nn.functional as F
 
+from . import synth as S
 from .llama_ref import rope_inv_freq
+
+_MASK32 = (1 << 32) - 1
+
+
+def _u64(v: int) -> int:
+    """An unsigned 64-bit constant as the int64 with the same bits."""
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def _shr(x, k: int):
+    """Logical right shift of int64 tensors holding uint64 bit patterns."""
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def _splitmix64_(x):
+    """In place (int64 arithmetic wraps mod 2^64 like uint64)."""
+    x.add_(_u64(0x9E3779B97F4A7C15))
+    x.bitwise_xor_(_shr(x, 30)).mul_(_u64(0xBF58476D1CE4E5B9))
+    x.bitwise_xor_(_shr(x, 27)).mul_(_u64(0x94D049BB133111EB))
+    return x.bitwise_xor_(_shr(x, 31))
+
+
+def synth_linear(seed: int, kind: int, layer: int, rows: int, cols: int, std: float, dtype=torch.bfloat16):
+    """oracle/synth.py ``linear`` in torch (all threads): the engine's counter-based weights,
+    bit for bit (tests/test_oracle.py checks against the numpy restatement)."""
+    sh = int(S.splitmix64(S.np.uint64(seed)))
+    scale = float(S.np.float32(std * S.np.sqrt(3.0) / 65536.0))
+    out = torch.empty(rows, cols, dtype=dtype)
+    c = torch.arange(cols, dtype=torch.int64)[None, :]
+    step = max(1, (1 << 20) // cols)
+    for r0 in range(0, rows, step):
+        r = torch.arange(r0, min(rows, r0 + step), dtype=torch.int64)[:, None]
+        h = ((r << 20) | c).bitwise_or_((kind << 58) | (layer << 50)).bitwise_xor_(_u64(sh))
+        _splitmix64_(h)
+        lim = (h & 0xFFFF).add_((h >> 16) & 0xFFFF).add_((h >> 32) & 0xFFFF).add_(_shr(h, 48)).sub_(131070)
+        out[r0:r0 + r.shape[0]] = lim.to(torch.float32).mul_(scale).to(dtype)  # RNE, as bf16_rne
+    return out
+
+
+def synth_norm(seed: int, kind: int, layer: int, n: int, jitter: float, dtype=torch.bfloat16):
+    return torch.from_numpy(S.norm(seed, kind, layer, n, jitter)).to(dtype)
 
 
 class TorchCpuLlama:
-    def __init__(self, cfg, seed: int = 0, std: float = 0.02, dtype=torch.bfloat16):
-        self.cfg, self.dt = cfg, dtype
-        g = torch.Generator().manual_seed(seed)
-        H, D, F_ = cfg.hidden, cfg.head_dim, cfg.ffn
+    """The map call on the CPU, over the engine's own synthetic weights (ms_init_synthetic /
+    oracle/synth.py: same seed, std, norm jitter -> the same bf16 values)."""
 
-        def lin(r, c):
-            return (torch.randn(r, c, generator=g, dtype=torch.float32) * std).to(dtype)
-        self.embed = lin(cfg.vocab, H)
+    def __init__(self, cfg, seed: int = 0, std: float = 0.02, jitter: float = 0.0, dtype=torch.bfloat16):
+        self.cfg, self.dt = cfg, dtype
+        H, D, F_ = cfg.hidden, cfg.head_dim, cfg.ffn
+        QD, KD = cfg.n_heads * D, cfg.n_kv_heads * D
+
+        def lin(kind, layer, r, c):
+            return synth_linear(seed, kind, layer, r, c, std, dtype)
+        self.embed = lin(S.EMBED, 0, cfg.vocab, H)
+        self.lm_head = self.embed if cfg.tie_embeddings else lin(S.LM_HEAD, 0, cfg.vocab, H)
         self.layers = []
-        for _ in range(cfg.n_layers):
+        for l in range(cfg.n_layers):
             self.layers.append({
-                "wqkv": lin((cfg.n_heads + 2 * cfg.n_kv_heads) * D, H), "wo": lin(H, cfg.n_heads * D),
-                "wgu": lin(2 * F_, H), "wdown": lin(H, F_),
-                "n1": torch.ones(H, dtype=dtype), "n2": torch.ones(H, dtype=dtype)})
-        self.final_norm = torch.ones(H, dtype=dtype)
+                "wqkv": torch.cat([lin(S.WQ, l, QD, H), lin(S.WK, l, KD, H), lin(S.WV, l, KD, H)]),
+                "wo": lin(S.WO, l, H, QD),
+                "wgu": torch.cat([lin(S.WGATE, l, F_, H), lin(S.WUP, l, F_, H)]), "wdown": lin(S.WDOWN, l, H, F_),
+                "n1": synth_norm(seed, S.ATTN_NORM, l, H, jitter, dtype),
+                "n2": synth_norm(seed, S.FFN_NORM, l, H, jitter, dtype)})
+        self.final_norm = synth_norm(seed, S.FINAL_NORM, 0, H, jitter, dtype)
         self.inv_freq = torch.tensor(rope_inv_freq(cfg), dtype=torch.float64)
 
     def _rope(self, x, pos):
@@ -74,8 +122,8 @@ class TorchCpuLlama:
             gu = self._norm(x, L["n2"]) @ L["wgu"].T
             h = F.silu(gu[:, :cfg.ffn].float()) * gu[:, cfg.ffn:].float()
             x = x + (h.to(self.dt) @ L["wdown"].T).float()
-        xn = self._norm(x[-1:], self.final_norm)
-        return int(torch.argmax((xn @ self.embed.T).float(), -1))
+        self.last_logits = (self._norm(x[-1:], self.final_norm) @ self.lm_head.T).float()[0]
+        return int(torch.argmax(self.last_logits))
 
     def new_cache(self, max_ctx):
         c = self.cfg
@@ -83,11 +131,22 @@ class TorchCpuLlama:
                  torch.zeros(max_ctx, c.n_kv_heads, c.head_dim, dtype=self.dt)) for _ in range(c.n_layers)]
 
 
-def time_chunk(cfg, prompt_ids, gen_len: int, decode_sample: int = 16, seed: int = 0) -> dict:
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def time_chunk(cfg, prompt_ids, gen_len: int, decode_sample: int = 16, seed: int = 0, std: float = 0.02) -> dict:
     """Time one map call on the CPU: the full prefill of ``prompt_ids`` plus
     ``decode_sample`` greedy decode steps, extrapolated to ``gen_len`` generated tokens
-    (decode steps at this context length cost the same to within the KV growth)."""
-    m = TorchCpuLlama(cfg, seed=seed)
+    (decode steps at this context length cost the same to within the KV growth).  The weights
+    are the engine's (bench.py: ms_init_synthetic(seed 0, std 0.02, jitter 0))."""
+    m = TorchCpuLlama(cfg, seed=seed, std=std)
     ids = torch.as_tensor(prompt_ids, dtype=torch.long)
     P = ids.shape[0]
     cache = m.new_cache(P + gen_len)
@@ -101,4 +160,4 @@ def time_chunk(cfg, prompt_ids, gen_len: int, decode_sample: int = 16, seed: int
     t_dec = (time.perf_counter() - t0) / max(n, 1)
     chunk_s = t_pre + (gen_len - 1) * t_dec
     return {"prefill_s": t_pre, "decode_step_s": t_dec, "chunk_s": chunk_s,
-            "threads": torch.get_num_threads(), "decode_steps_timed": n}
+            "threads": torch.get_num_threads(), "decode_steps_timed": n, "cpu_model": cpu_model()}

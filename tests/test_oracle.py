@@ -84,3 +84,24 @@ def test_bf16_rounding_is_nearest_even():
     assert r.tolist()[:4] == [1.0, 1.0, 1.015625, -2.5]
     bits = synth.to_bf16_bits(r)
     assert np.array_equal(synth.from_bf16_bits(bits), r)
+
+
+def test_torch_cpu_baseline_is_the_same_model():
+    """bench.py's cpu_baseline (oracle/torch_cpu.py) runs the engine's own synthetic weights:
+    the torch generator is bit-exact with oracle/synth.py, and on TINY its last-position logits
+    follow the numpy oracle's (bf16 torch arithmetic vs the oracle's rounding points)."""
+    import torch
+    from mapsum.config import TINY
+    from oracle import synth as S
+    from oracle.llama_ref import OracleLlama
+    from oracle.torch_cpu import TorchCpuLlama, synth_linear
+    assert np.array_equal(synth_linear(5, S.WUP, 1, 64, 768, 0.05).float().numpy(), S.linear(5, S.WUP, 1, 64, 768, 0.05))
+    seed, std, jit = 3, 0.05, 0.1
+    m = TorchCpuLlama(TINY, seed=seed, std=std, jitter=jit)
+    o = OracleLlama(TINY, S.make_weights(TINY, seed, std=std, jitter=jit))
+    ids = np.random.default_rng(1).integers(0, 4000, size=80)
+    cache = m.new_cache(96)
+    m.forward(torch.as_tensor(ids), cache, 0)
+    ref, _ = o.forward(ids)
+    got = m.last_logits.numpy()
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 3e-2

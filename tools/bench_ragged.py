@@ -43,14 +43,25 @@ def main():
                 max_prefill_tokens=16384) as eng:
         eng.init_synthetic(seed=0, std=0.02, norm_jitter=0.0)
         eng.generate(prompts[:4], num_predict=8, ignore_eos=True)  # warm-up (graphs, caches)
-        times = []
+        times, outs = [], []
         for _ in range(args.reps):
             eng.synchronize()
             t0 = time.perf_counter()
             res = eng.generate(prompts, num_predict=args.gen_len, ignore_eos=True)
             eng.synchronize()
             times.append(time.perf_counter() - t0)
-        assert all(len(r.ids) == args.gen_len for r in res)
+            outs.append([r.ids for r in res])
+        st = eng.stats()
+        # self-checks outside the timed region (as bench.py): same summaries every repetition,
+        # full length, and a section's summary independent of its companions (the shortest,
+        # the median and the longest section rerun alone)
+        order = np.argsort(lens)
+        picks = [int(order[0]), int(order[len(order) // 2]), int(order[-1])]
+        alone = {i: eng.generate([prompts[i]], num_predict=args.gen_len, ignore_eos=True)[0].ids for i in picks}
+        check = {"deterministic_across_reps": all(o == outs[0] for o in outs[1:]),
+                 "full_length": all(len(x) == args.gen_len for x in outs[0]),
+                 "batch_invariant": all(alone[i] == outs[0][i] for i in picks)}
+        assert all(check.values()), check
     dt = min(times)
     print(json.dumps({
         "metric": "hierarchical level: ragged sections/s (configs[3])", "value": round(args.sections / dt, 3),
@@ -59,7 +70,8 @@ def main():
         "config": {"sections": args.sections, "max_batch": args.max_batch, "gen_len": args.gen_len,
                    "prompt_tokens": {"min": int(lens.min()), "median": int(np.median(lens)),
                                      "max": int(lens.max()), "sum": int(lens.sum())},
-                   "weights": "bf16 synthetic", "n_gpus": 1}}), flush=True)
+                   "weights": "bf16 synthetic", "n_gpus": 1},
+        "graphs_built": st["graphs_built"], "check": check}), flush=True)
 
 
 if __name__ == "__main__":
