@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -106,7 +107,7 @@ struct ms_engine {
   bf16_t *kpool = nullptr, *vpool = nullptr;
   size_t layer_kv_elems = 0;
   int32_t* bt_d = nullptr;
-  std::vector<int32_t> bt_h;
+  int32_t* bt_h = nullptr;  // pinned host copy of the block table (async row uploads)
   std::vector<int> free_pages, free_slots;
   float* x = nullptr;
   bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
@@ -137,7 +138,7 @@ struct ms_engine {
   // of QKV / gate-up blocks loads x and the statistics before its weight stream starts (+10 /
   // +7.5 us per launch against the 2 x 4.9 us norm launches it removes), so it stays off
   // (profiles/r03/v1_norm_fused_ab.txt).
-  bool norm_fuse = false, has_quant = false;  // MS_NORM_FUSED=1: measured slower, see below
+  bool norm_fuse = false, has_quant = false, warned_quant_large = false;  // MS_NORM_FUSED=1: measured slower, see below
   int norm_rt = 12, ssq_tiles = 0;
   float* ssq = nullptr;
   static constexpr int kNormMaxBatch = 10;
@@ -164,6 +165,34 @@ struct ms_engine {
   int32_t* args_d = nullptr;
   int32_t* args_h = nullptr;  // pinned
   size_t args_cap = 0;
+  // Prefill and decode each own a stream, activations, argument staging, first-token /
+  // argmax buffers and timing events, so the prefill of newly admitted chunks runs on one
+  // stream WHILE the decode run of the running chunks runs on the other (prefill is
+  // MFMA-bound, decode HBM-bound: SURVEY.md §7 step 6 "admit prefill chunks while decoding").
+  // use() points the working members (stream, x, xb, ..., ev_a/ev_b) at one of them; KV pages,
+  // slots and weights are shared (a chunk's pages are only touched by its own phase).
+  // Measured on MI355X (configs[2], 128 slots, profiles/r03/v3_overlap_*): the two phases
+  // interfere -- the prefill GEMMs and the decode step's short launches share every CU, so
+  // prefill took +28 % and a decode step +23 % -- and the whole job was 8 % SLOWER with a
+  // 16-step run under each prefill (2.6 % slower with one-step runs), natural EOS or not.  So
+  // the phases run one after the other by default; MS_OVERLAP=1 turns the overlap on.
+  struct Ctx {
+    hipStream_t stream = nullptr;
+    float* x = nullptr;
+    bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
+    float* logits = nullptr;
+    int32_t* ids_out_d = nullptr;
+    int32_t* args_d = nullptr;
+    int32_t* args_h = nullptr;
+    size_t args_cap = 0;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  } cp, cd;
+  bool overlap = false;
+  void use(const Ctx& c) {
+    stream = c.stream; x = c.x; xb = c.xb; qkv = c.qkv; attn = c.attn; hbuf = c.hbuf;
+    logits = c.logits; ids_out_d = c.ids_out_d; args_d = c.args_d; args_h = c.args_h;
+    args_cap = c.args_cap; ev_a = c.ev_a; ev_b = c.ev_b;
+  }
   std::vector<uint8_t> stop_set;  // ms_set_eos_ids: a stop-id bitmap replacing cfg.eos_ids
   std::deque<std::unique_ptr<Seq>> waiting;
   std::vector<std::unique_ptr<Seq>> running;
@@ -187,6 +216,7 @@ struct ms_engine {
   int graph_steps = 16;
   bool use_graphs = true;
   int32_t* ids_host = nullptr;  // pinned landing buffer: kMaxRun steps x <= 256 greedy ids
+  int32_t* first_host = nullptr;  // pinned: the first greedy id of each prefilled prompt
   int32_t* ids_ring_d = nullptr;  // device ring of a decode run's ids (decode_advance)
   static constexpr int kMaxRun = 64;  // chained decode steps per host synchronisation
   int max_run = kMaxRun;              // MS_DECODE_RUN (1 = one step per ms_step)
@@ -598,9 +628,12 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     ms_engine& E = *e;
     E.cfg = *cfg;
     HIP_OK(hipSetDevice(cfg->device));
-    HIP_OK(hipStreamCreateWithFlags(&E.stream, hipStreamNonBlocking));
-    HIP_OK(hipEventCreate(&E.ev_a));
-    HIP_OK(hipEventCreate(&E.ev_b));
+    for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {
+      HIP_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+      HIP_OK(hipEventCreate(&c->ev_a));
+      HIP_OK(hipEventCreate(&c->ev_b));
+    }
+    E.use(E.cp);
     E.H = cfg->hidden; E.Hq = cfg->n_heads; E.Hk = cfg->n_kv_heads; E.D = cfg->head_dim;
     E.F = cfg->ffn; E.V = cfg->vocab; E.L = cfg->n_layers;
     E.QKVN = (E.Hq + 2 * E.Hk) * E.D;
@@ -633,19 +666,24 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.layer_kv_elems = (size_t)E.n_pages * E.Hk * kPage * E.D;
     E.kpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
     E.vpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
-    E.bt_h.assign((size_t)cfg->max_batch * E.max_pages, 0);
-    E.bt_d = E.dalloc<int32_t>(E.bt_h.size(), true);
+    HIP_OK(hipHostMalloc((void**)&E.bt_h, (size_t)cfg->max_batch * E.max_pages * sizeof(int32_t),
+                         hipHostMallocDefault));
+    std::memset(E.bt_h, 0, (size_t)cfg->max_batch * E.max_pages * sizeof(int32_t));
+    E.bt_d = E.dalloc<int32_t>((size_t)cfg->max_batch * E.max_pages, true);
     for (int p = E.n_pages - 1; p >= 0; --p) E.free_pages.push_back(p);
     for (int s = cfg->max_batch - 1; s >= 0; --s) E.free_slots.push_back(s);
     // activations
     const size_t T = E.Tmax;
-    E.x = E.dalloc<float>(T * E.H);
-    E.xb = E.dalloc<bf16_t>(T * E.H);
-    E.qkv = E.dalloc<bf16_t>(T * E.QKVN);
-    E.attn = E.dalloc<bf16_t>(T * E.Hq * E.D);
-    E.hbuf = E.dalloc<bf16_t>(T * E.F);
-    E.logits = E.dalloc<float>((size_t)cfg->max_batch * E.V);
-    E.ids_out_d = E.dalloc<int32_t>(cfg->max_batch);
+    for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {  // prefill: T rows; decode: max_batch rows
+      const size_t R = c == &E.cp ? T : (size_t)cfg->max_batch;
+      c->x = E.dalloc<float>(R * E.H);
+      c->xb = E.dalloc<bf16_t>(R * E.H);
+      c->qkv = E.dalloc<bf16_t>(R * E.QKVN);
+      c->attn = E.dalloc<bf16_t>(R * E.Hq * E.D);
+      c->hbuf = E.dalloc<bf16_t>(R * E.F);
+      c->logits = E.dalloc<float>((size_t)cfg->max_batch * E.V);
+      c->ids_out_d = E.dalloc<int32_t>(cfg->max_batch);
+    }
     const int Md = std::min(cfg->max_batch, 64);
     size_t gws = 0;
     const int shapes[5][2] = {{E.QKVN, E.H}, {E.H, E.Hq * E.D}, {2 * E.F, E.H}, {E.H, E.F}, {E.V, E.H}};
@@ -676,12 +714,17 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
                   E.H % E.split_qkv == 0;
     E.ssq = E.dalloc<float>((size_t)256 * std::max(cfg->max_batch, 16), true);
     if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
-    E.args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
-    E.args_d = E.dalloc<int32_t>(E.args_cap);
-    HIP_OK(hipHostMalloc((void**)&E.args_h, E.args_cap * sizeof(int32_t), hipHostMallocDefault));
+    for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {
+      c->args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
+      c->args_d = E.dalloc<int32_t>(c->args_cap);
+      HIP_OK(hipHostMalloc((void**)&c->args_h, c->args_cap * sizeof(int32_t), hipHostMallocDefault));
+    }
+    if (const char* v = getenv("MS_OVERLAP")) E.overlap = atoi(v) != 0;
+    E.use(E.cp);
     HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * 256 * sizeof(int32_t),
                          hipHostMallocDefault));
     E.ids_ring_d = E.dalloc<int32_t>((size_t)ms_engine::kMaxRun * 256);
+    HIP_OK(hipHostMalloc((void**)&E.first_host, (size_t)cfg->max_batch * sizeof(int32_t), hipHostMallocDefault));
     if (const char* v = getenv("MS_DECODE_RUN")) E.max_run = std::max(1, std::min(atoi(v), (int)ms_engine::kMaxRun));
     if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
     HIP_OK(hipDeviceSynchronize());
@@ -698,18 +741,24 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
 int ms_destroy(ms_engine* e) {
   if (!e) return MS_OK;
   (void)hipSetDevice(e->cfg.device);
-  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (ms_engine::Ctx* c : {&e->cp, &e->cd})
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (void* p : e->allocs) (void)hipFree(p);
-  if (e->args_h) (void)hipHostFree(e->args_h);
+  for (ms_engine::Ctx* c : {&e->cp, &e->cd})
+    if (c->args_h) (void)hipHostFree(c->args_h);
   if (e->ids_host) (void)hipHostFree(e->ids_host);
+  if (e->first_host) (void)hipHostFree(e->first_host);
+  if (e->bt_h) (void)hipHostFree(e->bt_h);
   for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
   for (auto& pe : e->ev_pairs) {
     (void)hipEventDestroy(pe.start);
     (void)hipEventDestroy(pe.stop);
   }
-  if (e->ev_a) (void)hipEventDestroy(e->ev_a);
-  if (e->ev_b) (void)hipEventDestroy(e->ev_b);
-  if (e->stream) (void)hipStreamDestroy(e->stream);
+  for (ms_engine::Ctx* c : {&e->cp, &e->cd}) {
+    if (c->ev_a) (void)hipEventDestroy(c->ev_a);
+    if (c->ev_b) (void)hipEventDestroy(c->ev_b);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+  }
   delete e;
   return MS_OK;
 }
@@ -1178,8 +1227,10 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   launch_argmax(E.logits, S, E.V, E.ids_out_d, E.stream);
   E.prof_end(K_MISC);
   HIP_OK(hipGetLastError());
+  // pinned landing buffer: a pageable destination would make this copy wait for the prefill
+  // on the host, before the overlapping decode run is launched
   first_ids->resize(S);
-  HIP_OK(hipMemcpyAsync(first_ids->data(), E.ids_out_d, S * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
+  HIP_OK(hipMemcpyAsync(E.first_host, E.ids_out_d, S * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
 }
 
 // kernels of one decode step (no host synchronisation: capturable into a hipGraph)
@@ -1287,7 +1338,10 @@ int ms_step(ms_engine* e) {
   return guarded(e, [&]() -> int {
     ms_engine& E = *e;
     HIP_OK(hipSetDevice(E.cfg.device));
-    // 1. admit
+    // Profiling runs serialise the phases, so every bracketed launch runs alone on the chip.
+    const bool ov = E.overlap && E.prof_mask == 0;
+    // 1. admit (the new slots' block-table rows go out on the prefill stream)
+    E.use(E.cp);
     std::vector<Seq*> admitted;
     int budget = E.cfg.max_prefill_tokens;
     while (!E.waiting.empty() && !E.free_slots.empty()) {
@@ -1301,37 +1355,55 @@ int ms_step(ms_engine* e) {
       E.running.push_back(std::move(E.waiting.front()));
       E.waiting.pop_front();
     }
-    // 2. prefill the admitted prompts
-    if (!admitted.empty()) {
-      std::vector<int32_t> first;
-      HIP_OK(hipEventRecord(E.ev_a, E.stream));
-      prefill(E, admitted, E.L, nullptr, &first);
-      HIP_OK(hipEventRecord(E.ev_b, E.stream));
-      HIP_OK(hipStreamSynchronize(E.stream));
+    // 2. prefill the admitted prompts on the prefill stream; with overlap the host does not
+    // wait here: the decode run below proceeds on the decode stream meanwhile, and the new
+    // chunks join the decode batch from the next step on
+    std::vector<int32_t> first;
+    auto finish_prefill = [&]() {
+      HIP_OK(hipStreamSynchronize(E.cp.stream));
       float ms_ = 0.f;
-      HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
+      HIP_OK(hipEventElapsedTime(&ms_, E.cp.ev_a, E.cp.ev_b));
       E.stats.prefill_ms += ms_;
-      E.prof_collect();
       E.stats.prefill_passes += 1;
       for (size_t i = 0; i < admitted.size(); ++i) {
         Seq& s = *admitted[i];
         s.len = (int)s.prompt.size();
         E.stats.prefill_tokens += s.len;
-        accept_token(E, s, first[i]);
+        accept_token(E, s, E.first_host[i]);
+      }
+    };
+    if (!admitted.empty()) {
+      HIP_OK(hipEventRecord(E.cp.ev_a, E.cp.stream));
+      prefill(E, admitted, E.L, nullptr, &first);
+      HIP_OK(hipEventRecord(E.cp.ev_b, E.cp.stream));
+      if (!ov) {
+        finish_prefill();
+        E.prof_collect();
       }
     }
-    // 3. decode every running sequence that still needs tokens: a run of k chained steps
-    // (one host synchronisation), k bounded by the nearest num_predict, the attention split
-    // grid and kMaxRun; k = 1 while admissible work waits for a free slot
+    // 3. decode every running sequence that still needs tokens and has been prefilled: a run
+    // of k chained steps (one host synchronisation), k bounded by the nearest num_predict, the
+    // attention split grid and kMaxRun; k = 1 while admissible work waits for a free slot
+    E.use(E.cd);
+    if (E.large_engine && E.has_quant && !E.warned_quant_large) {
+      // say so instead of silently changing arithmetic with the engine size
+      fprintf(stderr, "libmapsum: a %d-slot engine decodes in the large-batch regime: K-quant matrices are "
+              "multiplied from their bf16 dequantised copies (skinny MFMA GEMM); the exact fp32 K-quant GEMV "
+              "runs in engines of < %d slots\n", E.cfg.max_batch, E.dgemm_min);
+      E.warned_quant_large = true;
+    }
     std::vector<Seq*> batch;
     for (auto& s : E.running)
-      if (!s->finish) batch.push_back(s.get());
+      if (!s->finish && s->len > 0) batch.push_back(s.get());
     for (size_t i0 = 0; i0 < batch.size(); i0 += 256) {
       std::vector<Seq*> sub(batch.begin() + i0, batch.begin() + std::min(batch.size(), i0 + 256));
       int k = (batch.size() > 256 || (!E.waiting.empty() && !E.free_slots.empty())) ? 1 : E.max_run;
       // chunks wait for a slot: a chunk that stops at EOS inside the run keeps its slot until
       // the run ends, so bound the run by one captured graph (<= 16 steps) instead of 64
       if (!E.waiting.empty()) k = std::min(k, std::max(1, E.graph_steps));
+      // a prefill is in flight on the other stream: decode a whole graph of steps under it
+      // (a one-step run would leave the prefill exposed)
+      if (ov && !admitted.empty() && batch.size() <= 256) k = std::max(k, std::max(1, E.graph_steps));
       int max_len = 0;
       for (Seq* s : sub) {
         k = std::min(k, s->num_predict - (int)s->out.size());
@@ -1356,6 +1428,8 @@ int ms_step(ms_engine* e) {
           accept_token(E, s, ids[(size_t)j * sub.size() + i]);
         }
     }
+    if (ov && !admitted.empty()) finish_prefill();
+    E.use(E.cp);
     // 4. retire finished sequences
     for (auto it = E.running.begin(); it != E.running.end();) {
       if ((*it)->finish) {
@@ -1414,7 +1488,8 @@ int ms_set_profiling(ms_engine* e, uint32_t mask) {
 int ms_synchronize(ms_engine* e) {
   if (!e) return MS_EINVAL;
   return guarded(e, [&]() -> int {
-    HIP_OK(hipStreamSynchronize(e->stream));
+    HIP_OK(hipStreamSynchronize(e->cp.stream));
+    HIP_OK(hipStreamSynchronize(e->cd.stream));
     return MS_OK;
   });
 }
@@ -1439,6 +1514,7 @@ int ms_forward_packed(ms_engine* e, const int32_t* ids, const int32_t* lens, int
     REQUIRE(T <= E.cfg.max_prefill_tokens, MS_EINVAL, "probe longer than max_prefill_tokens");
     REQUIRE(pages <= (int64_t)E.free_pages.size(), MS_ENOSPC, "not enough KV pages");
     for (int64_t i = 0; i < T; ++i) REQUIRE(ids[i] >= 0 && ids[i] < E.V, MS_EINVAL, "token id out of range");
+    E.use(E.cp);
     std::vector<Seq> seqs(n_seqs);
     std::vector<Seq*> b;
     int64_t off = 0;

@@ -299,12 +299,10 @@ def test_qgemv_bench_shapes(dev, qtype, N, K, epi):
     assert float((out.double() - exp).norm() / exp.norm()) < tol
 
 
-@pytest.mark.timeout(900)
-def test_fullshape_q4_k_m_engine_vs_oracle(dev):
-    """configs[4] at the full widths (2 layers): Q4_K_M blocks through ms_load_weight_q;
-    prefill logits and 64 teacher-forced greedy tokens against the oracle run on the
-    dequantised weights."""
-    from mapsum.weights import load_quantized
+@pytest.fixture(scope="module")
+def q4km(dev):
+    """configs[4] weights at the full widths (2 layers): random Q4_K/Q6_K blocks in the Q4_K_M
+    mix, and the oracle on their bf16-rounded dequantisation."""
     from oracle import quants as Q
     from oracle.synth import bf16_rne
     H, D, F, V = CFG.hidden, CFG.head_dim, CFG.ffn, CFG.vocab
@@ -325,9 +323,21 @@ def test_fullshape_q4_k_m_engine_vs_oracle(dev):
             qw[(l, name)] = (qt, blk)
             ly[name] = bf16_rne(Q.dequant(blk, qt)).reshape(r, c)
         w["layers"].append(ly)
-    o = OracleLlama(CFG, w)
+    return qw, w, OracleLlama(CFG, w)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("slots", [2, 32])
+def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
+    """configs[4] at the full widths (2 layers): Q4_K_M blocks through ms_load_weight_q;
+    prefill logits and 64 teacher-forced greedy tokens against the oracle run on the
+    dequantised weights.  slots = 2: the dequant-fused K-quant GEMVs; slots = 32: the
+    large-batch regime, which multiplies the bf16 dequantised copies (tested, and
+    the engine says so on stderr)."""
+    from mapsum.weights import load_quantized
+    qw, w, o = q4km
     prompt = _chunks()[2][:768]
-    e = Engine(CFG, device=0, max_batch=2, max_ctx=1024, max_prefill_tokens=2048)
+    e = Engine(CFG, device=0, max_batch=slots, max_ctx=1024, max_prefill_tokens=2048)
     try:
         load_quantized(e, qw, w)
         _, lg = e.forward(prompt, hidden=False, logits=True)
@@ -342,8 +352,8 @@ def test_fullshape_q4_k_m_engine_vs_oracle(dev):
         srt = np.sort(tl, 1)
         top2 = srt[:, -1] - srt[:, -2]
         dec = top2 > DECISIVE * noise
-        print(f"q4_k_m: logits rel err {err:.3e}; teacher-forced {np.mean(want == gen):.4f}, decisive "
-              f"{dec.sum()} agree {np.mean(want[dec] == gen[dec]):.4f}")
+        print(f"q4_k_m ({slots} slots): logits rel err {err:.3e}; teacher-forced {np.mean(want == gen):.4f}, "
+              f"decisive {dec.sum()} agree {np.mean(want[dec] == gen[dec]):.4f}")
         for i in np.nonzero(want != gen)[0]:
             assert srt[i, -1] - tl[i, gen[i]] <= 1e-2 * (abs(srt[i, -1]) + 1.0)
         assert np.mean(want[dec] == gen[dec]) >= 0.99
