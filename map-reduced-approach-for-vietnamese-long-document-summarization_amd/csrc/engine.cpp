@@ -138,7 +138,8 @@ struct ms_engine {
   // of QKV / gate-up blocks loads x and the statistics before its weight stream starts (+10 /
   // +7.5 us per launch against the 2 x 4.9 us norm launches it removes), so it stays off
   // (profiles/r03/v1_norm_fused_ab.txt).
-  bool norm_fuse = false, has_quant = false, warned_quant_large = false;  // MS_NORM_FUSED=1: measured slower, see below
+  bool norm_fuse = false, has_quant = false, warned_quant_large = false;
+  bool resid_epi = false;  // MS_RESID_EPI=1: O / down add into x themselves (resid_proj)  // MS_NORM_FUSED=1: measured slower, see below
   int norm_rt = 12, ssq_tiles = 0;
   float* ssq = nullptr;
   static constexpr int kNormMaxBatch = 10;
@@ -433,7 +434,11 @@ struct ms_engine {
     prof_begin(K_ATTN_DECODE);
     launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
     prof_end(K_ATTN_DECODE);
-    pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
+    if (resid_epi && !large(B) && !Q[QS_O].ready()) {
+      resid_proj(attn, Ly.wo, B, H, Hq * D);
+    } else {
+      pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
+    }
     residual_norm(Ly.ffn_norm, B);
     if (large(B)) {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
@@ -448,7 +453,22 @@ struct ms_engine {
     } else {
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
     }
-    pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down, dsplit_down);
+    if (resid_epi && !large(B) && !Q[QS_DOWN].ready()) {
+      resid_proj(hbuf, Ly.wdown, B, H, F);
+    } else {
+      pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down, dsplit_down);
+    }
+  }
+
+  // x += X . W^T in the GEMV epilogue (no split-K slabs), on norm_rt-row tiles (256 blocks for
+  // the 3072-row O / down): the residual_rmsnorm after it then reads one row instead of S+1
+  void resid_proj(const bf16_t* X, const bf16_t* W, int B, int N, int K) {
+    GemvArgs g{};
+    g.rt = norm_rt;
+    prof_begin(K_GEMV);
+    launch_gemv_ex(X, W, x, B, N, K, N, MS_GEMV_EPI_ADD_F32, &g, 0, stream);
+    prof_end(K_GEMV);
+    pending_split = 0;
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each)
@@ -706,6 +726,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_PGEMV")) E.use_pgemv = atoi(v) != 0;
     if (cfg->max_batch > 16) E.use_pgemv = false;  // per engine: every step the same arithmetic
     if (const char* v = getenv("MS_PSPLIT")) E.psplit = std::max(1, atoi(v));
+    if (const char* v = getenv("MS_RESID_EPI")) E.resid_epi = atoi(v) != 0;
     if (E.H % E.norm_rt || E.H / E.norm_rt > 256) E.norm_rt = 16;
     E.norm_fuse = E.norm_fuse && E.H % E.norm_rt == 0 && E.H / E.norm_rt <= 256 &&
                   gemv_norm_supported(cfg->max_batch, E.QKVN, E.H / E.split_qkv, MS_GEMV_EPI_STORE_F32,
