@@ -41,8 +41,9 @@ class MapBackend:
     All engine calls run on one worker thread (the engine is not thread-safe); async
     callers are batched: every request queued before a scheduler tick joins it."""
 
-    def __init__(self, engine, tokenizer, template=render_llama32):
+    def __init__(self, engine, tokenizer, template=render_llama32, retries: int = 0):
         self.engine = engine
+        self.retries = retries    # re-queues of a MS_FINISH_ERROR chunk (see Engine.generate)
         self.tok = tokenizer
         self.template = template
         self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=1, thread_name_prefix="mapsum")
@@ -58,10 +59,10 @@ class MapBackend:
 
     # -- synchronous path (one chunk, or a list of chunks) ----------------------
     def generate_ids(self, id_lists, num_predict: int) -> list:
-        res = self._pool.submit(self.engine.generate, id_lists, num_predict).result()
+        res = self._pool.submit(self.engine.generate, id_lists, num_predict, False, self.retries).result()
         for r in res:
-            if r.finish == "error":  # failed twice (Engine.generate re-queues once)
-                raise RuntimeError("mapsum: chunk failed twice (no finite logit)")
+            if r.finish == "error":  # deterministic: a re-run would fail the same way
+                raise RuntimeError("mapsum: chunk failed (no finite logit)")
         return res
 
     def generate(self, prompts, num_predict: int) -> list:
@@ -83,7 +84,7 @@ class MapBackend:
             self._tag += 1
             tag = self._tag
         self._queue.append((tag, ids, num_predict))
-        self._inflight[tag] = (fut, ids, num_predict, 1)  # one re-queue left
+        self._inflight[tag] = (fut, ids, num_predict, self.retries)
         if self._driver is None or self._driver.done():
             self._driver = asyncio.ensure_future(self._drive())
         r = await fut
@@ -121,14 +122,14 @@ class MapBackend:
                         continue
                     if r.finish != "error":
                         fut.set_result(r)
-                    elif retries > 0:  # a failed chunk is re-queued once
+                    elif retries > 0:  # opt-in re-queue (transient device faults only)
                         with self._lock:
                             self._tag += 1
                             tag = self._tag
                         self._queue.append((tag, ids, n))
                         self._inflight[tag] = (fut, ids, n, retries - 1)
                     else:
-                        fut.set_exception(RuntimeError("mapsum: chunk failed twice (no finite logit)"))
+                        fut.set_exception(RuntimeError("mapsum: chunk failed (no finite logit)"))
         except Exception as e:  # the engine itself failed: every waiter fails loudly
             for ent in self._inflight.values():
                 if not ent[0].done():

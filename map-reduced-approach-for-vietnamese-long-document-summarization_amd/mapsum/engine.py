@@ -57,12 +57,15 @@ class RequestQueue:
         mine = [t for t in self._mailbox if pred(t)]
         return [self._mailbox.pop(t) for t in mine]
 
-    def generate(self, prompts, num_predict: int, ignore_eos: bool = False, retries: int = 1) -> list:
+    def generate(self, prompts, num_predict: int, ignore_eos: bool = False, retries: int = 0) -> list:
         """Run every prompt (list of id lists) to completion; results in input order.
 
         A chunk that finishes with MS_FINISH_ERROR (no finite logit: SURVEY.md §5 failure
-        row) is re-queued ``retries`` times on its own; the rest of the batch is unaffected.
-        The reference has no retry at all (run_full_evaluation_pipeline.py:627-638)."""
+        row) fails alone; the rest of the batch is unaffected.  Greedy decoding is
+        deterministic and batch-invariant, so re-running such a chunk recomputes the same
+        non-finite logits: by default it is reported at once.  ``retries`` > 0 re-queues it
+        that many times, a guard against transient device faults only.  The reference has
+        no retry at all (run_full_evaluation_pipeline.py:627-638)."""
         tags = [self.submit(p, num_predict, ignore_eos) for p in prompts]
         order = {t: i for i, t in enumerate(tags)}
         left = {t: retries for t in tags}

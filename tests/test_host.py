@@ -172,14 +172,16 @@ def test_ollamallm_engine_error_is_raised(toy_tokenizer):
     compat._BACKENDS.pop("fake:broken")
 
 
-def test_generate_requeues_a_failed_chunk_once():
-    """a chunk finishing with MS_FINISH_ERROR is re-queued once; the others
-    are not re-run; a second failure is reported for that chunk alone."""
-    eng = FakeEngine(fail_first=[(1, 2, 3)])
-    res = eng.generate([[1, 2, 3], [4, 5]], num_predict=8)
-    assert [r.ids for r in res] == [[3, 2, 1], [5, 4]] and eng.batches == [2, 1]
+def test_generate_failed_chunk_fails_alone_and_retry_is_opt_in():
+    """a chunk finishing with MS_FINISH_ERROR fails alone and, by default, at
+    once (deterministic greedy decoding would recompute the same non-finite logits); with
+    retries=1 it is re-queued once and the others are not re-run."""
     eng = FakeEngine(fail_first=[(7,)])
-    assert eng.generate([[7], [8]], 4, retries=0)[0].finish == "error"
+    res = eng.generate([[7], [8]], 4)
+    assert res[0].finish == "error" and res[1].ids == [8] and eng.batches == [2]
+    eng = FakeEngine(fail_first=[(1, 2, 3)])
+    res = eng.generate([[1, 2, 3], [4, 5]], num_predict=8, retries=1)
+    assert [r.ids for r in res] == [[3, 2, 1], [5, 4]] and eng.batches == [2, 1]
 
 
 def test_generate_leaves_foreign_results_in_the_mailbox():
@@ -210,19 +212,25 @@ def test_async_refused_request_fails_alone(toy_tokenizer):
     assert isinstance(a, str) and isinstance(c, str)
 
 
-def test_async_failed_chunk_is_requeued_once(toy_tokenizer):
+def test_async_failed_chunk_fails_alone_and_retry_is_opt_in(toy_tokenizer):
     prompt = "Tóm tắt lỗi"
-    be = compat.MapBackend(FakeEngine(), toy_tokenizer)
-    ids = tuple(be.encode_prompt(prompt))
-    be.engine.fail_first = {ids}
-    compat.register_backend("fake:retry", be)
-    m = compat.OllamaLLM("u", "fake:retry", max_new_tokens=1000)
-    try:
-        out = asyncio.run(m.ainvoke(prompt))
-    finally:
-        compat._BACKENDS.pop("fake:retry", None)
-    assert out == clean_thinking_tokens(toy_tokenizer.decode(list(ids)[::-1]))
-    assert be.engine.steps == 2
+    for retries in (0, 1):
+        be = compat.MapBackend(FakeEngine(), toy_tokenizer, retries=retries)
+        ids = tuple(be.encode_prompt(prompt))
+        be.engine.fail_first = {ids}
+        compat.register_backend("fake:retry", be)
+        m = compat.OllamaLLM("u", "fake:retry", max_new_tokens=1000)
+        try:
+            if retries == 0:  # default: the deterministic failure is reported once, at once
+                with pytest.raises(RuntimeError, match="no finite logit"):
+                    asyncio.run(m.ainvoke(prompt))
+                assert be.engine.steps == 1
+                continue
+            out = asyncio.run(m.ainvoke(prompt))
+        finally:
+            compat._BACKENDS.pop("fake:retry", None)
+        assert out == clean_thinking_tokens(toy_tokenizer.decode(list(ids)[::-1]))
+        assert be.engine.steps == 2
 
 
 # ------------------------------------------------------------------ chunk sharding
