@@ -216,12 +216,18 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
 /* tuning hook: ms_op_gemv over X [M][ldk] and W [N][ldk] (row stride ldk >= K elements) */
 int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                        int32_t ldk, int32_t ldo, int32_t epilogue, void* stream);
-/* persistent decode GEMV (one block per CU walking its 16-row tiles with the next tile's weights
-   in flight): epilogue MS_EPI_STORE_F32 into split-K slabs [S][M][N] (ldo = N), or MS_EPI_SWIGLU
-   with S = 1 (out bf16 [M][ldo = N/2]); M <= 16, (K/S) % 64 == 0.  Same sums as ms_op_gemv_split
-   (S slices) / ms_op_gemv (SwiGLU), bit for bit. */
-int ms_op_pgemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
-                int32_t ldo, int32_t epilogue, void* stream);
+/* decode O / down with the residual update fused (the engine's small-regime layer): x fp32
+   [M][N] += X . W^T on rt-row tiles (N % rt == 0, tiles = N / rt <= 256), and the input of the
+   next normalised projection: xg_out bf16 [M][N] = bf16(x * gamma), ssq_out fp32 [tiles][M] =
+   per-tile sums of the new x^2 (its deferred RMSNorm statistics, see ms_op_set_row_scale) */
+int ms_op_gemv_resid(const void* X, const void* W, float* x, void* xg_out, const void* gamma,
+                     float* ssq_out, int32_t M, int32_t N, int32_t K, int32_t rt, void* stream);
+/* the deferred RMSNorm of the numerics contract: the next ms_op_gemm /
+   ms_op_gemv / ms_op_gemv_split / ms_op_dgemm / ms_op_qgemv / ms_op_qgemv_split calls of the
+   calling thread scale output row r by 1/sqrt(sum_t ssq[t][r] / hidden + eps) (ssq [tiles][M];
+   gemm / dgemm: tiles == 1); ssq = NULL turns the scale off.  Test hook: the engine passes the
+   scale with each launch. */
+int ms_op_set_row_scale(const float* ssq, int32_t tiles, int32_t hidden, float eps);
 /* large-batch decode GEMM (M <= 256 rows; 64 weight rows per block, X shared via LDS): the
    ms_op_gemv epilogues (plus MS_EPI_ARGMAX); S > 1: split-K fp32 slabs [S][M][N] with
    epilogue MS_EPI_STORE_F32; N % 64 == 0, K % (64 S) == 0 */
@@ -231,9 +237,10 @@ int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, i
    waves = 0 picks the heuristic (tuning hook otherwise) */
 int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
                      int32_t S, int32_t waves, void* stream);
-/* x fp32 [rows][hidden] += slab_0 + ... + slab_{S-1} (slab order); y bf16 = rmsnorm(x) * w */
-int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y,
-                           int32_t rows, int32_t hidden, float eps, void* stream);
+/* x fp32 [rows][hidden] += slab_0 + ... + slab_{S-1} (slab order); then the input of the
+   normalised projection that follows: y bf16 = bf16(x * w), ssq[r] = sum of x[r]^2 (one tile) */
+int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y, float* ssq,
+                           int32_t rows, int32_t hidden, void* stream);
 /* K-quant ops: raw ggml blocks -> fp32 (bit-exact restatement of llama.cpp's
    dequantize_row_q4_K/q6_K); raw rows -> bf16 rows + packed rows (Q6_K repacked to 224 B);
    dequant-fused GEMV over packed rows (same epilogues as ms_op_gemv) */
@@ -246,8 +253,10 @@ int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void*
    (the quantised counterpart of ms_op_gemv_split; K % (256*S) == 0) */
 int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows, float* slabs,
                       int32_t M, int32_t N, int32_t K, int32_t S, void* stream);
-/* y bf16 [rows][hidden] = rmsnorm(x fp32 [.][hidden]) * w; row_idx optional gather */
-int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
+/* the input of a normalised projection: y bf16 [rows][hidden] = bf16(x * w) and ssq[r] = sum
+   of x[r]^2 over x fp32 [.][hidden] rows (row_idx optional gather); the projection then scales
+   its output rows by 1/sqrt(ssq / hidden + eps) (ms_op_set_row_scale) */
+int ms_op_rmsnorm(const void* x, const void* w, void* y, float* ssq, int32_t rows, int32_t hidden,
                   const int32_t* row_idx, void* stream);
 /* ids[r] = argmax_j logits[r][j] (ties -> lowest j; -1 when no logit of the row is finite) */
 int ms_op_argmax(const void* logits, int32_t rows, int32_t n, int32_t* ids, void* stream);

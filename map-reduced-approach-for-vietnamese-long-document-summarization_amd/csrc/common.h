@@ -72,31 +72,4 @@ __device__ __forceinline__ float wave_max(float v) {
 
 __device__ __forceinline__ void wait_vmcnt0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// In-launch hand-off words (cdna_hip_programming.md §6 Guideline 16, counter form with
-// write-through payload): every handed-off word is stored and loaded sc1 (relaxed agent-scope
-// atomics on GLOBAL pointers), every storing wave drains vmcnt before the workgroup barrier,
-// one lane adds to the counter, the block whose add returns count-1 is the reducer.
-typedef __attribute__((address_space(1))) unsigned gu32_t;
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store((gu32_t*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __uint_as_float(__hip_atomic_load((gu32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-// all storing waves drained + one arrival; true in every thread of the last arriving block.
-// flag: one LDS word no thread reads or writes otherwise during the call.
-__device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned count, unsigned* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned t = __hip_atomic_fetch_add((gu32_t*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (t == count - 1) ? 1u : 0u;
-  }
-  __syncthreads();
-  const bool last = *flag != 0u;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the sc1 loads below
-  return last;
-}
-
-
 }  // namespace ms

@@ -110,6 +110,7 @@ struct ms_engine {
   int32_t* bt_h = nullptr;  // pinned host copy of the block table (async row uploads)
   std::vector<int> free_pages, free_slots;
   float* x = nullptr;
+  float* ssq = nullptr;
   bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
   float* logits = nullptr;
   int32_t* ids_out_d = nullptr;
@@ -129,40 +130,28 @@ struct ms_engine {
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
-  // norm-fused decode (engines of <= kNormMaxBatch slots, bf16 weights; MS_NORM_FUSED=1): no
-  // residual_rmsnorm launches -- O and down run unsplit on norm_rt-row tiles (3072 / 12
-  // = 256 workgroups) and add into the fp32 residual themselves, writing per-tile sums of squares
-  // (ssq [tiles][B]); QKV and gate/up build their X as bf16(rmsnorm(x) * g) in their own
-  // prologue from those sums (k_gemv.hip kXNorm).  Chosen per engine, like the regimes above.
-  // Measured on MI355X at B = 8: 2.57 vs 2.25 ms per decode step -- every one of the hundreds
-  // of QKV / gate-up blocks loads x and the statistics before its weight stream starts (+10 /
-  // +7.5 us per launch against the 2 x 4.9 us norm launches it removes), so it stays off
-  // (profiles/r03/v1_norm_fused_ab.txt).
-  bool norm_fuse = false, has_quant = false, warned_quant_large = false;
-  bool resid_epi = false;  // MS_RESID_EPI=1: O / down add into x themselves (resid_proj)  // MS_NORM_FUSED=1: measured slower, see below
-  int norm_rt = 12, ssq_tiles = 0;
-  float* ssq = nullptr;
-  static constexpr int kNormMaxBatch = 10;
-  bool norm_fused() const {
-    return norm_fuse && !has_quant && !large_engine && cfg.max_batch <= kNormMaxBatch && attn_slabs;
+  // Residual-fused decode (small-regime engines, bf16 O / down): O and down run unsplit on
+  // resid_rt-row tiles (3072 / 12 = 256 workgroups, one per CU) and their epilogue adds into
+  // the fp32 residual and emits the next projection's input itself -- xb = bf16(x * g_next)
+  // and per-tile sums of x^2 (ssq [256][B]) -- so the decode layer has no residual_rmsnorm
+  // launch: the deferred RMSNorm (kernels.h RowScale) scales the rows of the QKV / gate-up /
+  // lm_head outputs instead.  Chosen per engine (MS_RESID_FUSED=0: split-K slabs + norm
+  // launches, the K-quant and large-regime form).
+  bool resid_fuse = true, has_quant = false, warned_quant_large = false;
+  int resid_rt = 12;
+  bool resid_fused(const QSlot* q) const {
+    return resid_fuse && !large_engine && !(q && q->ready());
   }
   bool large(int) const { return large_engine; }
   // split count of every quantised slab projection (MS_QSPLIT; 0: as bf16): 4 measured best
   // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the bf16 splits (6 / 6 / 4), 2 / 3 / 8
   // slower (profiles/r02/v27_qsplit_sweep_q4_k_m.txt)
   int qsplit = 4;
-  // persistent decode GEMVs (k_gemv.hip pgemv_kernel: one block per CU walking its tiles) for
-  // the bf16 projections of small-regime engines: QKV / O / down as psplit-way split-K slabs
-  // (4: 5 / 3 / 3 tiles per block, evenly balanced over 256 CUs), gate/up + SwiGLU unsplit.
-  // Measured on MI355X at B = 8 (profiles/r03/v2_pgemv_ab.txt): slower on every projection
-  // (gate/up 21.1 vs 19.4 us, QKV / O 7.9 vs 7.0, down 12.9 vs 12.6; 2.357 vs 2.255 ms per
-  // decode step) -- one block per CU with two register stages keeps fewer bytes in flight than
-  // two co-resident one-tile blocks -- so one block per tile stays the default (MS_PGEMV=1: A/B).
-  bool use_pgemv = false;
-  int psplit = 4;
-  // decode attention variants (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
-  // epilogue, B <= 16), split combine inside the attention launch (else a second launch)
-  bool attn_slabs = true, attn_fused_combine = false;
+  // decode attention variant (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
+  // epilogue, B <= 16)
+  bool attn_slabs = true;
+  // the deferred RMSNorm scale of the rows now in xb (set by whoever wrote xb)
+  RowScale cur_rs{};
   int32_t* args_d = nullptr;
   int32_t* args_h = nullptr;  // pinned
   size_t args_cap = 0;
@@ -180,6 +169,7 @@ struct ms_engine {
   struct Ctx {
     hipStream_t stream = nullptr;
     float* x = nullptr;
+    float* ssq = nullptr;  // sums of x^2 behind xb: [rows] (norm kernels) or [256][rows] (RESID)
     bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
     float* logits = nullptr;
     int32_t* ids_out_d = nullptr;
@@ -190,7 +180,7 @@ struct ms_engine {
   } cp, cd;
   bool overlap = false;
   void use(const Ctx& c) {
-    stream = c.stream; x = c.x; xb = c.xb; qkv = c.qkv; attn = c.attn; hbuf = c.hbuf;
+    stream = c.stream; x = c.x; ssq = c.ssq; xb = c.xb; qkv = c.qkv; attn = c.attn; hbuf = c.hbuf;
     logits = c.logits; ids_out_d = c.ids_out_d; args_d = c.args_d; args_h = c.args_h;
     args_cap = c.args_cap; ev_a = c.ev_a; ev_b = c.ev_b;
   }
@@ -279,13 +269,20 @@ struct ms_engine {
     return v;
   }
 
+  // the deferred RMSNorm scale of rows whose sums of squares a norm kernel wrote (one tile)
+  RowScale norm_rs() const { return RowScale{ssq, 1, H, cfg.norm_eps}; }
+
+  // normalised (rs) or plain projection: the decode GEMV where it fits, else the MFMA GEMM
   void gemm_or_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                    int epi, bool decode, int cls) {
+                    int epi, bool decode, int cls, const RowScale* rs = nullptr) {
     prof_begin(cls);
-    if (decode && gemv_supported(M, N, K, epi))
-      launch_gemv(X, W, out, M, N, K, ldo, epi, gemv_ws, stream);
-    else
-      launch_gemm(X, W, out, M, N, K, ldo, epi, stream);
+    if (decode && gemv_supported(M, N, K, epi)) {
+      GemvArgs ga{};
+      if (rs) ga.rs = *rs;
+      launch_gemv_ex(X, W, out, M, N, K, ldo, epi, &ga, 0, stream);
+    } else {
+      launch_gemm(X, W, out, M, N, K, ldo, epi, stream, rs);
+    }
     prof_end(cls);
   }
 
@@ -300,8 +297,10 @@ struct ms_engine {
     prof_end(cls);
   }
 
-  // decode with fused epilogues: residual+norm, QKV+RoPE+KV-scatter, attention(+combine),
-  // O (split-K slabs), residual+norm, gate/up+SwiGLU, down (split-K slabs)
+  // decode with fused epilogues: QKV (split-K slabs, deferred norm scale) -> attention (folds
+  // the slabs, RoPE, KV write) -> O -> gate/up + SwiGLU -> down, where O and down either add
+  // into the residual and emit the next projection's input themselves (resid_fused) or write
+  // split-K slabs that a residual_rmsnorm launch folds
   bool fused_decode(int B) const {
     if (large(B))
       return B <= kMaxSlabRows && attn_slabs && residual_rmsnorm_supported(kMaxSplit, H) &&
@@ -313,111 +312,85 @@ struct ms_engine {
     return B <= kMaxGemvRows && residual_rmsnorm_supported(kMaxSplit, H) &&
            (attn_slabs ? gemv_split_supported(B, QKVN, H, 1) : gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
            gemv_split_supported(B, H, Hq * D, 1) && gemv_split_supported(B, H, F, 1) &&
+           (!resid_fuse || (gemv_supported(B, H, Hq * D, MS_GEMV_EPI_RESID_SSQ) &&
+                            gemv_supported(B, H, F, MS_GEMV_EPI_RESID_SSQ))) &&
            attn_decode_supported(B, Hq, Hk, max_pages * kPage);
   }
   static constexpr int kMaxGemvRows = 64, kMaxSlabRows = 256, kMaxSplit = 8;
 
-  // projection into fp32 partial slabs [S][M][N]; returns the number of slabs written
-  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int Sl) {
+  // normalised projection into fp32 partial slabs [S][M][N], rows scaled by cur_rs; returns
+  // the number of slabs written
+  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int Sl,
+                 const RowScale* rs) {
     prof_begin(K_GEMV);
+    GemvArgs ga{};
+    if (rs) ga.rs = *rs;
     int used = 1;
     if (large(M)) {  // skinny GEMM on the bf16 weights (K-quant copies included)
-      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream);
+      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
       used = Sl;
     } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
       // Q4_K/Q6_K: same split-K as bf16 (a 16-row tile carries 3.6x fewer weight bytes, so
       // the unsplit grid -- 192 blocks for O/down -- is too thin to cover 256 CUs)
       const int Sq = qsplit > 0 ? qsplit : S;
       if (Sq > 1 && Sq <= kMaxSplit && qgemv_split_supported(M, N, K, Sq)) {
-        launch_qgemv_split(X, q->m, slabs, M, N, K, Sq, stream);
+        launch_qgemv_split(X, q->m, slabs, M, N, K, Sq, stream, &ga);
         used = Sq;
       } else {
-        launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
+        launch_qgemv(X, q->m, slabs, M, N, K, N, MS_GEMV_EPI_STORE_F32, &ga, stream);
       }
-    } else if (use_pgemv && pgemv_supported(M, N, K, psplit, MS_GEMV_EPI_STORE_F32, false)) {
-      launch_pgemv(X, W, slabs, M, N, K, psplit, N, MS_GEMV_EPI_STORE_F32, nullptr, stream);
-      used = psplit;
     } else {
       if (!(S >= 1 && S <= kMaxSplit && gemv_split_supported(M, N, K, S))) S = 1;
-      launch_gemv_split(X, W, slabs, M, N, K, S, 0, stream);
+      launch_gemv_split(X, W, slabs, M, N, K, S, 0, stream, &ga);
       used = S;
     }
     prof_end(K_GEMV);
     return used;
   }
 
-  // fold pending slabs into x, then RMSNorm(x) * w -> xb
+  // fold pending slabs into x, then xb = bf16(x * w) and its one-tile statistics
   void residual_norm(const bf16_t* w, int B) {
     prof_begin(K_MISC);
-    launch_residual_rmsnorm(x, slabs, pending_split, w, xb, B, H, cfg.norm_eps, stream);
+    launch_residual_rmsnorm(x, slabs, pending_split, w, xb, ssq, B, H, stream);
     prof_end(K_MISC);
     pending_split = 0;
+    cur_rs = norm_rs();
   }
 
-  GemvArgs norm_args(const bf16_t* gamma) const {
-    GemvArgs g{};
-    g.xres = x;
-    g.ssq_in = ssq;
-    g.ssq_tiles = ssq_tiles;
-    g.gamma = gamma;
-    g.hdim = H;
-    g.eps = cfg.norm_eps;
-    return g;
-  }
-
-  // one layer of the norm-fused decode step (norm_fused()): 5 launches instead of 7
-  void run_layer_norm_fused(int l, int B, const DecodeAttnArgs& da) {
-    const Layer& Ly = layers[l];
-    KVView kv = kv_layer(l);
-    // QKV -> split-K slabs; each block normalises its slice of x with attn_norm first
-    GemvArgs gq = norm_args(Ly.attn_norm);
-    int sq = split_qkv;
-    prof_begin(K_GEMV);
-    if (use_pgemv && pgemv_supported(B, QKVN, H, psplit, MS_GEMV_EPI_STORE_F32, true)) {
-      launch_pgemv(xb, Ly.wqkv, slabs, B, QKVN, H, psplit, QKVN, MS_GEMV_EPI_STORE_F32, &gq, stream);
-      sq = psplit;
+  // the residual update of O / down: x += X . W^T, then the input of the next normalised
+  // projection (gain g_next) -- in the GEMV epilogue (resid_fused: RESID_SSQ on resid_rt-row
+  // tiles, 256 tiles of statistics) or as split-K slabs + one residual_rmsnorm launch
+  void resid_update(const QSlot* q, const bf16_t* X, const bf16_t* W, int B, int K, int S, int Sl,
+                    const bf16_t* g_next) {
+    if (resid_fused(q)) {
+      GemvArgs ga{};
+      ga.rt = resid_rt;
+      ga.ssq_out = ssq;
+      ga.gamma = g_next;
+      ga.xg_out = xb;
+      prof_begin(K_GEMV);
+      launch_gemv_ex(X, W, x, B, H, K, H, MS_GEMV_EPI_RESID_SSQ, &ga, 0, stream);
+      prof_end(K_GEMV);
+      pending_split = 0;
+      cur_rs = RowScale{ssq, H / resid_rt, H, cfg.norm_eps};
     } else {
-      launch_gemv_split(xb, Ly.wqkv, slabs, B, QKVN, H, split_qkv, 0, stream, &gq);
+      pending_split = proj_split(q, X, W, B, H, K, S, Sl, nullptr);
+      residual_norm(g_next, B);
     }
-    prof_end(K_GEMV);
-    DecodeQKV qa{nullptr, slabs, sq, cos_tab, sin_tab};
-    prof_begin(K_ATTN_DECODE);
-    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
-    prof_end(K_ATTN_DECODE);
-    // O: x += attn . Wo^T on norm_rt-row tiles, + the ffn norm's statistics
-    GemvArgs go{};
-    go.rt = norm_rt;
-    go.ssq_out = ssq;
-    prof_begin(K_GEMV);
-    launch_gemv_ex(attn, Ly.wo, x, B, H, Hq * D, H, MS_GEMV_EPI_RESID_SSQ, &go, 0, stream);
-    prof_end(K_GEMV);
-    ssq_tiles = (H + norm_rt - 1) / norm_rt;
-    GemvArgs gg = norm_args(Ly.ffn_norm);
-    prof_begin(K_GEMV);
-    if (use_pgemv && pgemv_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU, true))
-      launch_pgemv(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, &gg, stream);
-    else
-      launch_gemv_ex(xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, 0, stream);
-    prof_end(K_GEMV);
-    prof_begin(K_GEMV);
-    launch_gemv_ex(hbuf, Ly.wdown, x, B, H, F, H, MS_GEMV_EPI_RESID_SSQ, &go, 0, stream);
-    prof_end(K_GEMV);
   }
 
   void run_layer_fused_decode(int l, int B, const int32_t* tok_pos, const int32_t* tok_slot,
                               const DecodeAttnArgs& da) {
-    if (norm_fused()) {
-      run_layer_norm_fused(l, B, da);
-      return;
-    }
     const Layer& Ly = layers[l];
     KVView kv = kv_layer(l);
-    residual_norm(Ly.attn_norm, B);
     const auto& Q = lq[l];
-    DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab};
+    const RowScale rs_attn = cur_rs;
+    DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab, rs_attn};
     if (attn_slabs) {
-      // QKV -> slabs; attention adds them, applies RoPE and writes the new K/V (k_attn.hip)
-      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv, dsplit_qkv);
+      // QKV -> unscaled slabs; attention adds them, applies the row's deferred-norm factor and
+      // RoPE, and writes the new K/V (k_attn.hip): one factor per attention block, not per
+      // QKV tile
+      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv, dsplit_qkv, nullptr);
     } else {
       // QKV GEMV epilogue: RoPE, q -> qkv rows, K/V -> paged cache
       GemvArgs ga{};
@@ -428,69 +401,50 @@ struct ms_engine {
       ga.kv = kv;
       ga.Hq = Hq;
       ga.Hk = Hk;
+      ga.rs = rs_attn;
       proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
-      qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab};
+      qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}};
     }
     prof_begin(K_ATTN_DECODE);
-    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream, attn_fused_combine);
+    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream);
     prof_end(K_ATTN_DECODE);
-    if (resid_epi && !large(B) && !Q[QS_O].ready()) {
-      resid_proj(attn, Ly.wo, B, H, Hq * D);
-    } else {
-      pending_split = proj_split(&Q[QS_O], attn, Ly.wo, B, H, Hq * D, split_o, dsplit_o);
-    }
-    residual_norm(Ly.ffn_norm, B);
+    resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm);
+    const RowScale rs_ffn = cur_rs;
     if (large(B)) {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
       prof_begin(K_GEMV);
-      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream);
-      prof_end(K_GEMV);
-    } else if (use_pgemv && !Q[QS_GU].ready() && pgemv_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU, false)) {
-      prof_begin(K_GEMV);
-      launch_pgemv(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, nullptr, stream);
+      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn);
       prof_end(K_GEMV);
     } else {
-      proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, nullptr, K_GEMV);
+      GemvArgs gg{};
+      gg.rs = rs_ffn;
+      proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV);
     }
-    if (resid_epi && !large(B) && !Q[QS_DOWN].ready()) {
-      resid_proj(hbuf, Ly.wdown, B, H, F);
-    } else {
-      pending_split = proj_split(&Q[QS_DOWN], hbuf, Ly.wdown, B, H, F, split_down, dsplit_down);
-    }
+    const bf16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
+    resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next);
   }
 
-  // x += X . W^T in the GEMV epilogue (no split-K slabs), on norm_rt-row tiles (256 blocks for
-  // the 3072-row O / down): the residual_rmsnorm after it then reads one row instead of S+1
-  void resid_proj(const bf16_t* X, const bf16_t* W, int B, int N, int K) {
-    GemvArgs g{};
-    g.rt = norm_rt;
-    prof_begin(K_GEMV);
-    launch_gemv_ex(X, W, x, B, N, K, N, MS_GEMV_EPI_ADD_F32, &g, 0, stream);
-    prof_end(K_GEMV);
-    pending_split = 0;
-  }
-
-  // one transformer layer over T packed tokens (decode: T = B rows, one token each)
+  // one transformer layer over T packed tokens (decode: T = B rows, one token each); on entry
+  // xb = bf16(x * attn_norm) with cur_rs, on exit xb = bf16(x * g_next) with cur_rs
+  // (tail = false: the last layer of a prefill whose caller normalises only the rows it needs)
   void run_layer(int l, int T, bool decode, const int32_t* tok_pos, const int32_t* tok_slot,
-                 const PrefillAttnArgs& pa, const DecodeAttnArgs& da) {
+                 const PrefillAttnArgs& pa, const DecodeAttnArgs& da, bool tail = true) {
     if (decode && fused_decode(T)) {
       run_layer_fused_decode(l, T, tok_pos, tok_slot, da);
       return;
     }
     const Layer& Ly = layers[l];
     const int kc = decode ? K_GEMV : K_GEMM;
-    prof_begin(K_MISC);
-    launch_rmsnorm(x, Ly.attn_norm, xb, T, H, cfg.norm_eps, nullptr, stream);
-    prof_end(K_MISC);
-    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_BF16, decode, kc);
+    const RowScale rs_attn = cur_rs;
+    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_BF16, decode, kc, &rs_attn);
     KVView kv = kv_layer(l);
     prof_begin(K_MISC);
     launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
     prof_end(K_MISC);
     if (decode) {
       prof_begin(K_ATTN_DECODE);
-      launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab}, attn, Hq, Hk, kv, da, attn_ws, stream);
+      launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}}, attn, Hq, Hk, kv, da, attn_ws, stream);
       prof_end(K_ATTN_DECODE);
     } else {
       prof_begin(K_ATTN_PREFILL);
@@ -498,11 +452,19 @@ struct ms_engine {
       prof_end(K_ATTN_PREFILL);
     }
     gemm_or_gemv(attn, Ly.wo, x, T, H, Hq * D, H, MS_EPI_ADD_F32, decode, kc);
-    prof_begin(K_MISC);
-    launch_rmsnorm(x, Ly.ffn_norm, xb, T, H, cfg.norm_eps, nullptr, stream);
-    prof_end(K_MISC);
-    gemm_or_gemv(xb, Ly.wgu, hbuf, T, 2 * F, H, F, MS_EPI_SWIGLU, decode, kc);
+    norm_input(Ly.ffn_norm, T);
+    const RowScale rs_ffn = cur_rs;
+    gemm_or_gemv(xb, Ly.wgu, hbuf, T, 2 * F, H, F, MS_EPI_SWIGLU, decode, kc, &rs_ffn);
     gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
+    if (tail) norm_input(l + 1 < L ? layers[l + 1].attn_norm : final_norm, T);
+  }
+
+  // xb = bf16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
+  void norm_input(const bf16_t* w, int T, const int32_t* row_idx = nullptr) {
+    prof_begin(K_MISC);
+    launch_rmsnorm(x, w, xb, ssq, T, H, row_idx, stream);
+    prof_end(K_MISC);
+    cur_rs = norm_rs();
   }
 
   // K-quant tensors loaded so far, (tensor, layer, ggml type) in load order: the manifest a
@@ -697,6 +659,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {  // prefill: T rows; decode: max_batch rows
       const size_t R = c == &E.cp ? T : (size_t)cfg->max_batch;
       c->x = E.dalloc<float>(R * E.H);
+      c->ssq = E.dalloc<float>(std::max(R, (size_t)256 * cfg->max_batch), true);
       c->xb = E.dalloc<bf16_t>(R * E.H);
       c->qkv = E.dalloc<bf16_t>(R * E.QKVN);
       c->attn = E.dalloc<bf16_t>(R * E.Hq * E.D);
@@ -710,30 +673,20 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     for (auto& sh : shapes) gws = std::max(gws, gemv_workspace_bytes(Md, sh[0], sh[1]));
     E.gemv_ws = E.dalloc<char>(gws, true);
     E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
-                                       true);  // zeroed: split-combine tickets
+                                       true);
     E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * std::min(std::max(cfg->max_batch, 64), 256) *
                               std::max(E.QKVN, E.H));
     if (const char* v = getenv("MS_SPLIT_QKV")) E.split_qkv = atoi(v);
     if (const char* v = getenv("MS_ATTN_SLABS")) E.attn_slabs = atoi(v) != 0;
-    if (const char* v = getenv("MS_ATTN_FUSED_COMBINE")) E.attn_fused_combine = atoi(v) != 0;
     if (const char* v = getenv("MS_SPLIT_O")) E.split_o = atoi(v);
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
-    if (const char* v = getenv("MS_NORM_FUSED")) E.norm_fuse = atoi(v) != 0;
-    if (const char* v = getenv("MS_PGEMV")) E.use_pgemv = atoi(v) != 0;
-    if (cfg->max_batch > 16) E.use_pgemv = false;  // per engine: every step the same arithmetic
-    if (const char* v = getenv("MS_PSPLIT")) E.psplit = std::max(1, atoi(v));
-    if (const char* v = getenv("MS_RESID_EPI")) E.resid_epi = atoi(v) != 0;
-    if (E.H % E.norm_rt || E.H / E.norm_rt > 256) E.norm_rt = 16;
-    E.norm_fuse = E.norm_fuse && E.H % E.norm_rt == 0 && E.H / E.norm_rt <= 256 &&
-                  gemv_norm_supported(cfg->max_batch, E.QKVN, E.H / E.split_qkv, MS_GEMV_EPI_STORE_F32,
-                                      256, 0) &&
-                  gemv_norm_supported(cfg->max_batch, 2 * E.F, E.H, MS_GEMV_EPI_SWIGLU, 256, 0) &&
-                  E.H % E.split_qkv == 0;
-    E.ssq = E.dalloc<float>((size_t)256 * std::max(cfg->max_batch, 16), true);
+    if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
+    if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
+    if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
     if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
     for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {
       c->args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
@@ -1225,24 +1178,24 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   E.prof_begin(K_MISC);
   launch_embed(d + o_ids, T, E.embed, E.H, E.x, E.stream);
   E.prof_end(K_MISC);
-  for (int l = 0; l < n_layers_run; ++l) E.run_layer(l, T, false, d + o_pos, d + o_slot, pa, da);
+  E.norm_input(E.layers[0].attn_norm, T);
+  for (int l = 0; l < n_layers_run; ++l)
+    E.run_layer(l, T, false, d + o_pos, d + o_slot, pa, da, l + 1 < E.L || logits_all);
   HIP_OK(hipGetLastError());
   if (n_layers_run < E.L) return;
   if (!logits_all && !first_ids) return;  // probe of the final residual only
-  if (logits_all) {  // probe: logits of every position
-    launch_rmsnorm(E.x, E.final_norm, E.xb, T, E.H, E.cfg.norm_eps, nullptr, E.stream);
-    launch_gemm(E.xb, E.lm_head, logits_all, T, E.V, E.H, E.V, MS_EPI_STORE_F32, E.stream);
+  if (logits_all) {  // probe: logits of every position (xb = bf16(x * final_norm), cur_rs)
+    launch_gemm(E.xb, E.lm_head, logits_all, T, E.V, E.H, E.V, MS_EPI_STORE_F32, E.stream, &E.cur_rs);
     return;
   }
-  E.prof_begin(K_MISC);
-  launch_rmsnorm(E.x, E.final_norm, E.xb, S, E.H, E.cfg.norm_eps, d + o_last, E.stream);
-  E.prof_end(K_MISC);
+  E.norm_input(E.final_norm, S, d + o_last);
   // the first token goes through the decode lm_head GEMV in row groups of <= 64: its sum
   // order is then the decode steps' one whatever the number of admitted prompts
   for (int r0 = 0; r0 < S; r0 += ms_engine::kMaxGemvRows) {
     const int rows = std::min(S - r0, (int)ms_engine::kMaxGemvRows);
+    const RowScale rs{E.ssq + r0, 1, E.H, E.cfg.norm_eps};
     E.gemm_or_gemv(E.xb + (size_t)r0 * E.H, E.lm_head, E.logits + (size_t)r0 * E.V, rows, E.V, E.H, E.V,
-                   MS_EPI_STORE_F32, true, K_LMHEAD);
+                   MS_EPI_STORE_F32, true, K_LMHEAD, &rs);
   }
   E.prof_begin(K_MISC);
   launch_argmax(E.logits, S, E.V, E.ids_out_d, E.stream);
@@ -1258,19 +1211,18 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
 static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& da) {
   const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
   PrefillAttnArgs pa{};
-  // in-launch split-combine counters start at zero every step (a memset node)
-  if (E.attn_fused_combine) HIP_OK(hipMemsetAsync(E.attn_ws, 0, attn_decode_ticket_bytes(), E.stream));
   E.prof_begin(K_MISC);
-  const bool nf = E.norm_fused() && E.fused_decode(B);
-  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream, nf ? E.ssq : nullptr);
+  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
   E.prof_end(K_MISC);
-  E.ssq_tiles = 1;  // the embedding's per-row sums of squares
   E.pending_split = 0;
+  E.residual_norm(E.layers[0].attn_norm, B);
+  // every layer leaves xb = bf16(x * the next gain) with its deferred scale in cur_rs
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
-  E.residual_norm(E.final_norm, B);  // folds the last layer's down slabs (if fused)
+  const RowScale rs = E.cur_rs;
   if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX)) {
     const int tiles = E.V / 16;
     E.prof_begin(K_LMHEAD);
+    // no row scale: r > 0 keeps every row's order (the logits themselves are never stored)
     launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream);
     E.prof_end(K_LMHEAD);
     E.prof_begin(K_MISC);
@@ -1284,7 +1236,7 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
     E.prof_end(K_MISC);
   } else {
-    E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD);
+    E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD, &rs);
     E.prof_begin(K_MISC);
     launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
     E.prof_end(K_MISC);
@@ -1588,12 +1540,28 @@ static int op_guard(const std::function<void()>& fn) {
   }
 }
 
+// the deferred RMSNorm scale the next op calls of this thread apply (ms_op_set_row_scale)
+static thread_local RowScale g_op_rs{};
+
+int ms_op_set_row_scale(const float* ssq, int32_t tiles, int32_t hidden, float eps) {
+  if (ssq && (tiles < 1 || hidden < 1)) return MS_EINVAL;
+  g_op_rs = ssq ? RowScale{ssq, tiles, hidden, eps} : RowScale{};
+  return MS_OK;
+}
+
+static const GemvArgs* op_gemv_args(GemvArgs& ga) {
+  ga = GemvArgs{};
+  ga.rs = g_op_rs;
+  return g_op_rs.ssq ? &ga : nullptr;
+}
+
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t ldo,
                int32_t epi, void* stream) {
   return op_guard([&] {
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
-    launch_gemm((const bf16_t*)A, (const bf16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream);
+    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "gemm row scale: one-tile statistics only");
+    launch_gemm((const bf16_t*)A, (const bf16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }
 
@@ -1620,7 +1588,8 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0),
             MS_EINVAL, "bad epilogue");
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
-    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, nullptr, waves,
+    GemvArgs ga;
+    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, op_gemv_args(ga), waves,
                    (hipStream_t)stream);
   });
 }
@@ -1636,13 +1605,19 @@ int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32
   });
 }
 
-int ms_op_pgemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K, int32_t S,
-                int32_t ldo, int32_t epi, void* stream) {
+int ms_op_gemv_resid(const void* X, const void* W, float* x, void* xg_out, const void* gamma,
+                     float* ssq_out, int32_t M, int32_t N, int32_t K, int32_t rt, void* stream) {
   return op_guard([&] {
-    REQUIRE(X && W && out, MS_EINVAL, "bad pgemv operands");
-    REQUIRE(pgemv_supported(M, N, K, S, epi, false), MS_EINVAL,
-            "pgemv shape unsupported (M <= 16; STORE_F32 slabs or SWIGLU with S = 1; (K/S) % 64 == 0)");
-    launch_pgemv((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, nullptr, (hipStream_t)stream);
+    REQUIRE(X && W && x && xg_out && gamma && ssq_out && rt >= 1 && rt <= 16 && N % rt == 0, MS_EINVAL,
+            "bad gemv_resid operands");
+    REQUIRE(gemv_supported(M, N, K, MS_GEMV_EPI_RESID_SSQ), MS_EINVAL, "gemv_resid shape unsupported");
+    GemvArgs ga{};
+    ga.rt = rt;
+    ga.ssq_out = ssq_out;
+    ga.gamma = (const bf16_t*)gamma;
+    ga.xg_out = (bf16_t*)xg_out;
+    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, x, M, N, K, N, MS_GEMV_EPI_RESID_SSQ, &ga, 0,
+                   (hipStream_t)stream);
   });
 }
 
@@ -1652,7 +1627,8 @@ int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, i
     REQUIRE(X && W && out, MS_EINVAL, "bad dgemm operands");
     REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && dgemm_supported(M, N, K, S, epi), MS_EINVAL,
             "dgemm shape unsupported (M <= 256, N % 64 == 0, K % (64 S) == 0, S > 1 only for fp32 slabs)");
-    launch_dgemm((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, (hipStream_t)stream);
+    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "dgemm row scale: one-tile statistics only");
+    launch_dgemm((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }
 
@@ -1661,19 +1637,21 @@ int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int3
   return op_guard([&] {
     REQUIRE(X && W && slabs && N >= 16 && S >= 1, MS_EINVAL, "bad gemv_split operands");
     REQUIRE(gemv_split_supported(M, N, K, S), MS_EINVAL, "gemv_split shape unsupported (M<=64, (K/S)%64==0)");
-    launch_gemv_split((const bf16_t*)X, (const bf16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream);
+    GemvArgs ga;
+    launch_gemv_split((const bf16_t*)X, (const bf16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream,
+                      op_gemv_args(ga));
   });
 }
 
-int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y,
-                           int32_t rows, int32_t hidden, float eps, void* stream) {
+int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y, float* ssq,
+                           int32_t rows, int32_t hidden, void* stream) {
   return op_guard([&] {
-    REQUIRE(x && w && y && rows >= 1 && hidden >= 4 && hidden % 4 == 0 && hidden <= 8192, MS_EINVAL,
+    REQUIRE(x && w && y && ssq && rows >= 1 && hidden >= 4 && hidden % 4 == 0 && hidden <= 8192, MS_EINVAL,
             "bad residual_rmsnorm shape");
     REQUIRE(S == 0 || slabs, MS_EINVAL, "slabs missing");
     REQUIRE(residual_rmsnorm_supported(S, hidden) || (S == 0 && hidden <= 8192), MS_EINVAL,
             "residual_rmsnorm: S <= 8 and hidden <= 3072 (wider rows: S == 0 only)");
-    launch_residual_rmsnorm(x, slabs, S, (const bf16_t*)w, (bf16_t*)y, rows, hidden, eps,
+    launch_residual_rmsnorm(x, slabs, S, (const bf16_t*)w, (bf16_t*)y, ssq, rows, hidden,
                             (hipStream_t)stream);
   });
 }
@@ -1710,7 +1688,8 @@ int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int3
     q.row0_0 = 0;
     q.type0 = type;
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
-    launch_qgemv((const bf16_t*)X, q, out, M, N, K, ldo, epi, nullptr, (hipStream_t)stream);
+    GemvArgs ga;
+    launch_qgemv((const bf16_t*)X, q, out, M, N, K, ldo, epi, op_gemv_args(ga), (hipStream_t)stream);
   });
 }
 
@@ -1726,15 +1705,17 @@ int ms_op_qgemv_split(const void* X, int32_t type, const void* packed, float* sl
     q.row0_0 = 0;
     q.type0 = type;
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
-    launch_qgemv_split((const bf16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream);
+    GemvArgs ga;
+    launch_qgemv_split((const bf16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream, op_gemv_args(ga));
   });
 }
 
-int ms_op_rmsnorm(const void* x, const void* w, void* y, int32_t rows, int32_t hidden, float eps,
+int ms_op_rmsnorm(const void* x, const void* w, void* y, float* ssq, int32_t rows, int32_t hidden,
                   const int32_t* row_idx, void* stream) {
   return op_guard([&] {
-    REQUIRE(x && w && y && rows >= 1 && hidden >= 4 && hidden % 4 == 0, MS_EINVAL, "bad rmsnorm shape");
-    launch_rmsnorm((const float*)x, (const bf16_t*)w, (bf16_t*)y, rows, hidden, eps, row_idx,
+    REQUIRE(x && w && y && ssq && rows >= 1 && hidden >= 4 && hidden % 4 == 0 && hidden <= 8192, MS_EINVAL,
+            "bad rmsnorm shape");
+    launch_rmsnorm((const float*)x, (const bf16_t*)w, (bf16_t*)y, ssq, rows, hidden, row_idx,
                    (hipStream_t)stream);
   });
 }

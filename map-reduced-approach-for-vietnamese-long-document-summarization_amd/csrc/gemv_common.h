@@ -6,17 +6,9 @@ namespace ms {
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *(const uint4*)p; }
 
-// once-read decode streams (weights, KV pages): non-temporal loads when MS_NT_STREAM is set
-// (MI355X_MICROARCH.md 'nt-weights': a decode weight stream read once per step)
-__device__ __forceinline__ uint4 ldw16(const void* p) {
-#ifdef MS_NT_STREAM
-  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-  const v4u v = __builtin_nontemporal_load((const v4u*)p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *(const uint4*)p;
-#endif
-}
+// once-read decode weight streams: plain loads (non-temporal ones measured slower on the whole
+// decode step, 2.45 vs 2.29 ms, profiles/r01 v5_nt_stream_ab_rejected)
+__device__ __forceinline__ uint4 ldw16(const void* p) { return *(const uint4*)p; }
 
 // s_waitcnt immediate for vmcnt(n) with expcnt/lgkmcnt left alone (gfx9 encoding)
 __host__ __device__ constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
@@ -54,65 +46,53 @@ __device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict_
   }
 }
 
-// where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip);
-// kXNorm: the LDS image of bf16(rmsnorm(x) * gamma), built by the block itself (gemv_norm_x)
-enum { kXGlobal = 0, kXLds = 1, kXRegs = 2, kXNorm = 3 };
-constexpr int kNormChunks = 4;  // float4 chunks of x per thread and pass (kXNorm prologue)
+// where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip)
+enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
 
-// The RMSNorm of the decode step, folded into the GEMV that consumes it (no norm launch):
-// xn[r][k] = bf16((x[r][k] * rinv[r]) * gamma[k]) for the block's K slice [k0, k0+K), written
-// into the X LDS image (x_lds layout), rinv[r] = 1/sqrt(sum_t ssq[t][r] / hdim + eps) from the
-// per-tile sums of squares of the RESID_SSQ producer.  Summation order is fixed (per lane
-// t = lane, +64, +128, +192 in sequence, then the wave tree) and per row, so a row's norm does
-// not depend on M or on the other rows.  Runs before the weight stream, in passes of
-// kNormChunks float4 per thread (the first pass's loads issued ahead of the statistics), so it
-// adds no registers to the GEMV body.  Needs ssq_tiles <= 256.
-__device__ __forceinline__ void gemv_norm_x(char* smem, const GemvArgs& ga, int M, int K, int k0) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const int nth = blockDim.x, KC = K >> 2, nch = M * KC;
-  float* rinv = (float*)(smem + gemv_x_lds_bytes(M, K));
-  typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-  f32x4 xv[kNormChunks];
-  u32x2 gv[kNormChunks];
-  auto load = [&](int base) {
-#pragma unroll
-    for (int i = 0; i < kNormChunks; ++i) {
-      const int c = min(base + tid + i * nth, nch - 1);
-      const int r = c / KC, cc = c - r * KC;
-      xv[i] = *(const f32x4*)(ga.xres + (size_t)r * ga.hdim + k0 + 4 * cc);
-      gv[i] = *(const u32x2*)(ga.gamma + k0 + 4 * cc);
+// The deferred RMSNorm scale of a GEMV block's output rows (kernels.h RowScale).  The partial
+// sums [tiles][M] are copied into LDS by DMA at the very start of the kernel, ahead of the X copy
+// and the weight stream (no registers: a register preload cost the 1024-thread gate/up GEMV its
+// second co-resident block), and folded after the stream into rinv[row], which the epilogue
+// reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order, then the
+// wave's xor tree.  Blocks with more than kRsStage partial sums read them from global memory
+// in the epilogue instead -- the same summation order, one memory round trip later.
+constexpr int kRsStage = 4096;  // floats of partial sums a block stages in LDS (16 KiB)
+__host__ __device__ inline int rs_stage_floats(const RowScale& rs, int M) {
+  const int n = rs.tiles * M;
+  return (rs.ssq && n <= kRsStage) ? (n + 63) / 64 * 64 : 0;
+}
+// LDS of a decode GEMV block: [main: the X image or the per-wave partials, whichever is larger]
+// [rinv: 64 floats][staged partial sums]
+__host__ __device__ inline size_t gemv_rinv_offset(size_t main_bytes) { return (main_bytes + 15) / 16 * 16; }
+__host__ __device__ inline size_t gemv_lds_total(size_t main_bytes, const RowScale& rs, int M) {
+  return gemv_rinv_offset(main_bytes) + 64 * 4 + (size_t)rs_stage_floats(rs, M) * 4;
+}
+__device__ __forceinline__ void rs_dma(char* smem, size_t rinv_off, const RowScale& rs, int M) {
+  const int nf = rs_stage_floats(rs, M);
+  if (nf == 0) return;  // block-uniform
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, n = rs.tiles * M;
+  float* stage = (float*)(smem + rinv_off) + 64;
+  for (int p = threadIdx.x >> 6; p * 64 < nf; p += nw)
+    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(p * 64 + lane, n - 1)),
+                                     (LDS_AS void*)(stage + p * 64), 4, 0, 0);
+}
+// every wave calls this after a barrier that follows the DMA's completion (vmcnt); rinv[row]
+// for row < M once the caller's next barrier has passed
+__device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, const RowScale& rs, int M) {
+  if (!rs.ssq) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  float* rinv = (float*)(smem + rinv_off);
+  const float* stage = rinv + 64;
+  const bool staged = rs_stage_floats(rs, M) > 0;
+  for (int row = wave; row < M; row += nw) {
+    float sum = 0.f;
+    for (int t = lane; t < ((rs.tiles + 63) & ~63); t += 64) {
+      const int i = t * M + row;
+      sum += t < rs.tiles ? (staged ? stage[i] : rs.ssq[i]) : 0.f;
     }
-  };
-  load(0);
-  for (int r = wave; r < M; r += nw) {
-    float v[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int t = lane + 64 * i;
-      v[i] = t < ga.ssq_tiles ? ga.ssq_in[(size_t)t * M + r] : 0.f;
-    }
-    const float sum = wave_sum(((v[0] + v[1]) + v[2]) + v[3]);
-    if (lane == 0) rinv[r] = 1.0f / sqrtf(sum / (float)ga.hdim + ga.eps);
+    sum = wave_sum(sum);
+    if (lane == 0) rinv[row] = rs_rinv(sum, rs);
   }
-  __syncthreads();
-  for (int base = 0; base < nch; base += kNormChunks * nth) {
-    if (base > 0) load(base);
-#pragma unroll
-    for (int i = 0; i < kNormChunks; ++i) {
-      const int c = base + tid + i * nth;
-      if (c < nch) {
-        const int r = c / KC, cc = c - r * KC;
-        const float ri = rinv[r];
-        const float g0 = __uint_as_float(gv[i].x << 16), g1 = __uint_as_float(gv[i].x & 0xFFFF0000u);
-        const float g2 = __uint_as_float(gv[i].y << 16), g3 = __uint_as_float(gv[i].y & 0xFFFF0000u);
-        uint2 o;
-        o.x = pack2bf((xv[i].x * ri) * g0, (xv[i].y * ri) * g1);
-        o.y = pack2bf((xv[i].z * ri) * g2, (xv[i].w * ri) * g3);
-        *(uint2*)(smem + x_lds(r, 4 * cc, K) + (cc & 1) * 8) = o;
-      }
-    }
-  }
-  __syncthreads();
 }
 
 constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave may hold (<= 32 VGPRs)
@@ -143,16 +123,19 @@ __device__ __forceinline__ void amax_merge_dev(float& v, int& i, float v2, int i
 // Cross-wave reduction of the per-wave MFMA accumulators through LDS and the epilogue.
 // acc[m][n][j] = C[row m*16 + 4*(lane>>4) + j][col n0 + n*16 + (lane&15)].
 template <int MT, int NT, int EPI>
-__device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, int ldo,
+__device__ __forceinline__ void gemv_epilogue(const float* red, const float* rinv, int M, int N, int ldo,
                                               void* __restrict__ out, int n0, const GemvArgs& ga);
 
 template <int MT, int NT, int EPI>
-__device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, int M, int N,
-                                            int ldo, void* __restrict__ out, int n0,
+__device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, size_t rinv_off,
+                                            int M, int N, int ldo, void* __restrict__ out, int n0,
                                             const GemvArgs& ga) {
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float* rinv = (const float*)(smem + rinv_off);
+  if (ga.rs.ssq) wait_vmcnt0();  // the staged partial sums (rs_dma) have landed
   __syncthreads();  // X image no longer needed: reuse LDS for the partials
+  rs_finish(smem, rinv_off, ga.rs, M);
   float* red = (float*)smem;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -160,16 +143,18 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
     for (int n = 0; n < NT; ++n)
       *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
   __syncthreads();
-  gemv_epilogue<MT, NT, EPI>(red, M, N, ldo, out, n0, ga);
+  gemv_epilogue<MT, NT, EPI>(red, rinv, M, N, ldo, out, n0, ga);
 }
 
 // The epilogue of a decode GEMV tile from the per-wave partials in LDS (red[wave][elem]).
 template <int MT, int NT, int EPI>
-__device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, int ldo,
+__device__ __forceinline__ void gemv_epilogue(const float* red, const float* rinv, int M, int N, int ldo,
                                               void* __restrict__ out, int n0, const GemvArgs& ga) {
   constexpr int ELEMS = MT * NT * 256;
   const int tid = threadIdx.x;
   const int nthreads = blockDim.x, nw = nthreads >> 6;
+  const bool scaled = ga.rs.ssq != nullptr;  // block-uniform
+  auto rsc = [&](int row) { return scaled ? rinv[row] : 1.0f; };
   // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
   auto sum_e = [&](int e) {
     float v = 0.f;
@@ -181,8 +166,9 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
       const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
       const int row = m * 16 + 4 * (l >> 4) + j;
       if (row >= M || n0 >= N) continue;
-      const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j);
-      const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j);
+      const float rv = rsc(row);
+      const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j) * rv;
+      const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j) * rv;
       const int f = (n0 >> 5) * 16 + (l & 15);
       ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(g / (1.0f + __expf(-g)) * u);
     }
@@ -197,8 +183,9 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
       const int t = (n0 % kHeadDim) / 16;
       for (int e = tid; e < M * 8; e += nthreads) {
         const int row = e >> 3, c = e & 7, i = 8 * t + c;
-        const float lo = bf2f(f2bf(sum_e(e_of(row, c))));      // q/k rounded to bf16, then
-        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8))));  // rotated in fp32 (as prefill)
+        const float rv = rsc(row);
+        const float lo = bf2f(f2bf(sum_e(e_of(row, c)) * rv));      // q/k rounded to bf16, then
+        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8)) * rv));  // rotated in fp32 (as prefill)
         const int pos = ga.tok_pos[row];
         const float cs = ga.cos_tab[(size_t)pos * 64 + i], sn = ga.sin_tab[(size_t)pos * 64 + i];
         const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
@@ -221,7 +208,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
         const int pos = ga.tok_pos[row], slot = ga.tok_slot[row];
         const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
         ga.kv.v[(((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim + d0 + c] =
-            f2bf(sum_e(e_of(row, c)));
+            f2bf(sum_e(e_of(row, c)) * rsc(row));
       }
     }
   } else if constexpr (EPI == MS_GEMV_EPI_RESID_SSQ) {
@@ -237,6 +224,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
         const float xo = *px + sum_e(e);
         *px = xo;
         q = xo * xo;
+        if (ga.xg_out) ga.xg_out[(size_t)row * ldo + col] = f2bf(xo * bf2f(ga.gamma[col]));
       }
 #pragma unroll
       for (int o = 4; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
@@ -248,7 +236,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
     for (int e = tid; e < ELEMS; e += nthreads) {
       const int m = e >> 8, l = (e >> 2) & 63, j = e & 3;
       const int row = m * 16 + 4 * (l >> 4) + j, col = n0 + (l & 15);
-      float v = (row < M && col < N) ? sum_e(e) : -INFINITY;
+      float v = (row < M && col < N) ? sum_e(e) * rsc(row) : -INFINITY;
       if (!(v == v)) v = -INFINITY;  // NaN never wins
       int idx = col;
 #pragma unroll
@@ -265,9 +253,9 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, int M, int N, in
       if (row >= M || col >= N || (NT == 1 && ga.rt > 0 && (l & 15) >= ga.rt)) continue;
       const float v = sum_e(e);
       const size_t o = (size_t)row * ldo + col;
-      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v);
+      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v * rsc(row));
       else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += v;
-      else ((float*)out)[o] = v;
+      else ((float*)out)[o] = v * rsc(row);
     }
   }
 }

@@ -63,14 +63,9 @@ __device__ __forceinline__ bf16x8 pack_p_lo(const f32x4& a, const f32x4& b, bf16
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-// decode KV pages are read once per step: non-temporal when MS_NT_STREAM is set
-__device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) {
-#ifdef MS_NT_STREAM
-  return __builtin_nontemporal_load((const u32x4*)p);
-#else
-  return *(const u32x4*)p;
-#endif
-}
+// decode KV pages (plain loads: non-temporal ones measured slower, 2.45 vs 2.29 ms per decode
+// step, profiles/r01 v5_nt_stream_ab_rejected)
+__device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) { return *(const u32x4*)p; }
 
 // ============================================================ prefill (varlen, causal)
 // 1-D grid over (q-block, head group), heaviest q-blocks first for every head group; block
@@ -333,29 +328,23 @@ static int decode_nsplit_max(int max_len) {
   return (np + kSplitPages * ppw_min - 1) / (kSplitPages * ppw_min);
 }
 
-constexpr int kMaxTickets = 4096;  // (b, kv head) pairs per launch
 constexpr int kMaxSplits = 127;
 
-// workspace: [tickets: kMaxTickets u32, zero at allocation, reset by each last arriver]
-//            [partials: (b, q head, split) x 132 floats]
+// workspace: partials (b, q head, split) x 132 floats {m, l, o[128], pad}
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len) {
-  return (size_t)kMaxTickets * 4 + (size_t)B * Hq * decode_nsplit_max(max_len) * 132 * sizeof(float);
+  return (size_t)B * Hq * decode_nsplit_max(max_len) * 132 * sizeof(float);
 }
 
-size_t attn_decode_ticket_bytes() { return (size_t)kMaxTickets * 4; }
-
 bool attn_decode_supported(int B, int Hq, int Hk, int max_len) {
-  return Hk >= 1 && Hq % Hk == 0 && Hq / Hk <= kMaxGroup && B * Hk <= kMaxTickets &&
-         decode_nsplit_max(max_len) <= kMaxSplits;
+  (void)B;
+  return Hk >= 1 && Hq % Hk == 0 && Hq / Hk <= kMaxGroup && decode_nsplit_max(max_len) <= kMaxSplits;
 }
 
 // PPWT = 2: the page loop unrolled for exactly 2 pages per wave (the B = 8 plan); 0: runtime
-template <bool FROM_SLABS, bool FUSED_COMBINE, int PPWT>
+template <bool FROM_SLABS, int PPWT>
 __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
                                                           DecodeAttnArgs a, float* __restrict__ ws,
-                                                          unsigned* __restrict__ tickets,
-                                                          bf16_t* __restrict__ out, int nsplit,
-                                                          int ppw, float scale_log2) {
+                                                          int nsplit, int ppw, float scale_log2) {
   __shared__ __attribute__((aligned(16))) char smem[4 * 16384 + (kMaxGroup + 2) * kHeadDim * 2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
@@ -416,6 +405,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     const float rsn = qa.sin_tab[(size_t)pos * 64 + (tid & 63)];
     const int nvec = (G + (owns_new ? 2 : 0)) * kHeadDim;
     constexpr int PER = ((kMaxGroup + 2) * kHeadDim + 255) / 256;
+    // the row's deferred-norm partial sums (every wave folds them itself: no extra barrier),
+    // lane l holding tiles l + 64 i in order -- gemv_common.h rs_finish's summation order
+    float rv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (qa.rs.ssq) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = lane + 64 * i;
+        rv[i] = t < qa.rs.tiles ? qa.rs.ssq[(size_t)t * a.B + b] : 0.f;
+      }
+    }
     float sv[PER][kMaxSlabs];  // every slab load of this thread in flight at once
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
@@ -427,6 +426,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
       for (int q = 0; q < kMaxSlabs; ++q) sv[i][q] = src[min(q, qa.S - 1) * sstride + col];
     }
+    const float rrow = qa.rs.ssq ? rs_rinv(wave_sum(((rv[0] + rv[1]) + rv[2]) + rv[3]), qa.rs) : 1.0f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int e = tid + i * 256;
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
       for (int q = 1; q < kMaxSlabs; ++q)
         if (q < qa.S) acc += sv[i][q];
-      if (e < nvec) raw[e] = bf2f(f2bf(acc));
+      if (e < nvec) raw[e] = bf2f(f2bf(acc * rrow));
     }
     __syncthreads();
     const int nrot = (G + (owns_new ? 1 : 0)) * 64;  // (head, i) pairs: the q heads, then k
@@ -581,63 +581,14 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     }
     const int hq = kvh * G + c;
     float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;
-    if constexpr (FUSED_COMBINE)
-      st_sc1(dst + k, (k == 0) ? M : acc);  // write-through: read by the last arriver below
-    else
-      dst[k] = (k == 0) ? M : acc;
-  }
-
-  // ---- in-launch combine: the last of the nsplit blocks of (b, kvh) merges the partials
-  // (Guideline 16 counter form with write-through partials: no fences; the counters are
-  // zeroed by a memset node ahead of the launch, and reset by the last arriver)
-  if constexpr (!FUSED_COMBINE) return;
-  unsigned* flag = (unsigned*)(smem + 4 * 16384);  // reuse qn (consumed)
-  if (!arrive_last(&tickets[b * Hk + kvh], (unsigned)nsplit, flag)) return;
-  if (tid == 0) __hip_atomic_store(&tickets[b * Hk + kvh], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // split weights per q head: f_s = 2^(m_s - max m), L = sum_s f_s l_s (split order)
-  float* ml = (float*)smem;                           // [G][128] m_s, then [G][128] l_s
-  float* wsum = ml + 2 * kMaxGroup * 128;             // [G][128] f_s, [c][127] = L
-  for (int e = tid; e < G * nsplit; e += 256) {       // every (head, split) load in parallel
-    const int c = e / nsplit, s_ = e - c * nsplit;
-    const float* p = ws + (((size_t)b * Hq + kvh * G + c) * nsplit + s_) * 132;
-    ml[c * 128 + s_] = ld_sc1(p);
-    ml[(kMaxGroup + c) * 128 + s_] = ld_sc1(p + 1);
-  }
-  __syncthreads();
-  for (int c = tid; c < G; c += 256) {
-    float M = -INFINITY;
-    for (int s_ = 0; s_ < nsplit; ++s_) M = fmaxf(M, ml[c * 128 + s_]);
-    float L = 0.f;
-    for (int s_ = 0; s_ < nsplit; ++s_) {
-      const float ms_ = ml[c * 128 + s_];
-      const float f = (ms_ == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ms_ - M);
-      wsum[c * 128 + s_] = f;
-      L += f * ml[(kMaxGroup + c) * 128 + s_];
-    }
-    wsum[c * 128 + 127] = L;
-  }
-  __syncthreads();
-  for (int e = tid; e < G * kHeadDim; e += 256) {
-    const int c = e >> 7, d = e & 127;
-    const float* p = ws + ((size_t)b * Hq + kvh * G + c) * nsplit * 132 + 2 + d;
-    const float* f = wsum + c * 128;
-    float O = 0.f;
-    if (nsplit <= 16) {  // clamped indices, no branches: all loads in flight at once
-      float ov[16];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) ov[q] = ld_sc1(p + min(q, nsplit - 1) * 132);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) O += (q < nsplit) ? f[q] * ov[q] : 0.f;
-    } else {
-      for (int q = 0; q < nsplit; ++q) O += f[q] * ld_sc1(p + q * 132);
-    }
-    out[(size_t)b * Hq * kHeadDim + (kvh * G + c) * kHeadDim + d] = f2bf(O / f[127]);
+    dst[k] = (k == 0) ? M : acc;
   }
 }
 
-// separate split combine (the default): out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s,
-// w_s = 2^(m_s - max m) -- measured cheaper on MI355X than the in-launch ticket combine,
-// whose release/acquire chain adds ~4 dependent memory round trips to every block
+// split combine: out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s, w_s = 2^(m_s - max m) --
+// its own launch (an in-launch ticket combine by the last-arriving split measured no faster:
+// 2.289 vs 2.294 ms per decode step, its release/acquire chain adds ~4 dependent memory round
+// trips to every block)
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
                                                                   bf16_t* __restrict__ out, int Hq,
                                                                   int nsplit) {
@@ -682,32 +633,28 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
 }
 
 void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
-                        DecodeAttnArgs a, float* ws, hipStream_t s, bool fused_combine) {
+                        DecodeAttnArgs a, float* ws, hipStream_t s) {
   if (a.B <= 0) return;
   if (!attn_decode_supported(a.B, Hq, Hk, a.max_len)) return;  // callers check
   if (qa.slabs && (qa.S < 1 || qa.S > kMaxSlabs)) return;
+  if (qa.slabs && qa.rs.ssq && (qa.rs.tiles < 1 || qa.rs.tiles > 256)) return;  // callers check
   const int ppw = a.ppw > 0 ? a.ppw : 2;
   const int nsplit = decode_nsplit(ppw, a.max_len);
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
-  unsigned* tickets = (unsigned*)ws;
-  ws = (float*)((char*)ws + (size_t)kMaxTickets * 4);
   const dim3 grid(a.B, Hk, nsplit);
-#define AD(SL, FC)                                                                                          \
+#define AD(SL)                                                                                              \
   do {                                                                                                      \
     if (ppw == 2)                                                                                           \
-      MS_LAUNCH((attn_decode_kernel<SL, FC, 2>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
-                nsplit, ppw, scale_log2);                                                                   \
+      MS_LAUNCH((attn_decode_kernel<SL, 2>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, nsplit, ppw,     \
+                scale_log2);                                                                                \
     else                                                                                                    \
-      MS_LAUNCH((attn_decode_kernel<SL, FC, 0>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, tickets, out, \
-                nsplit, ppw, scale_log2);                                                                   \
+      MS_LAUNCH((attn_decode_kernel<SL, 0>), grid, dim3(256), 0, s, qa, Hq, Hk, kv, a, ws, nsplit, ppw,     \
+                scale_log2);                                                                                \
   } while (0)
-  if (qa.slabs && fused_combine) AD(true, true);
-  else if (qa.slabs) AD(true, false);
-  else if (fused_combine) AD(false, true);
-  else AD(false, false);
+  if (qa.slabs) AD(true);
+  else AD(false);
 #undef AD
-  if (!fused_combine)
-    MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
+  MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
 }
 
 }  // namespace ms

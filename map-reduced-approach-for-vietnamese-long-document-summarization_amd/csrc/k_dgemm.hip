@@ -30,7 +30,7 @@ template <int MT, int EPI>
 __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16_t* __restrict__ X,
                                                       const bf16_t* __restrict__ W,
                                                       void* __restrict__ out, int M, int N, int K,
-                                                      int ldk, int ldo) {
+                                                      int ldk, int ldo, RowScale rs) {
   constexpr int DPF = dgemm_dpf<MT>();
   // one X stage: XR rows x 128 B (16*MT rounded up to whole 16-B chunks per thread)
   constexpr int XR = 16 * MT < 32 ? 32 : 16 * MT;
@@ -111,8 +111,15 @@ __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16
     }
   }
 
-  // epilogue: acc[m][j] = C[row m*16 + 4 fg + j][col n0 + 16 wave + fr]
+  // epilogue: acc[m][j] = C[row m*16 + 4 fg + j][col n0 + 16 wave + fr]; rows scaled by the
+  // deferred RMSNorm factor (one-tile RowScale: rs_rinv(ssq[row]), as every consumer forms it)
   const int col = n0 + 16 * wave + fr;
+  if (rs.ssq) {
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[m][j] *= rs_rinv(rs.ssq[min(m * 16 + 4 * fg + j, M - 1)], rs);
+  }
   if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
     // waves 2q / 2q+1 hold the gate / up tile of the same 16 features: pair through LDS
     float* xch = (float*)smem;  // [4 waves][MT][64 lanes][4]
@@ -172,11 +179,11 @@ bool dgemm_supported(int M, int N, int K, int S, int epi) {
 
 template <int MT>
 static void dgemm_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo,
-                     int epi, hipStream_t s) {
+                     int epi, const RowScale& rs, hipStream_t s) {
   const dim3 grid(N / DBN, S), blk(256);
   const int Ks = K / S;
   switch (epi) {
-#define DG(E_) MS_LAUNCH((dgemm_kernel<MT, E_>), grid, blk, 0, s, X, W, out, M, N, Ks, K, ldo)
+#define DG(E_) MS_LAUNCH((dgemm_kernel<MT, E_>), grid, blk, 0, s, X, W, out, M, N, Ks, K, ldo, rs)
     case MS_GEMV_EPI_STORE_BF16: DG(MS_GEMV_EPI_STORE_BF16); break;
     case MS_GEMV_EPI_ADD_F32: DG(MS_GEMV_EPI_ADD_F32); break;
     case MS_GEMV_EPI_SWIGLU: DG(MS_GEMV_EPI_SWIGLU); break;
@@ -186,15 +193,21 @@ static void dgemm_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, 
   }
 }
 
+// rs: the deferred RMSNorm scale of the output rows, one-tile partials only (or null)
 void launch_dgemm(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  hipStream_t s) {
+                  hipStream_t s, const RowScale* rs_in) {
   if (!dgemm_supported(M, N, K, S, epi)) return;  // callers check
+  RowScale rs{};
+  if (rs_in && rs_in->ssq && epi != MS_GEMV_EPI_ARGMAX) {  // argmax: r > 0 keeps the order
+    if (rs_in->tiles != 1) return;  // callers pass one-tile statistics (a norm kernel's)
+    rs = *rs_in;
+  }
   const int mt = (M + 15) / 16;
-  if (mt <= 1) dgemm_go<1>(X, W, out, M, N, K, S, ldo, epi, s);
-  else if (mt <= 2) dgemm_go<2>(X, W, out, M, N, K, S, ldo, epi, s);
-  else if (mt <= 4) dgemm_go<4>(X, W, out, M, N, K, S, ldo, epi, s);
-  else if (mt <= 8) dgemm_go<8>(X, W, out, M, N, K, S, ldo, epi, s);
-  else dgemm_go<16>(X, W, out, M, N, K, S, ldo, epi, s);
+  if (mt <= 1) dgemm_go<1>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+  else if (mt <= 2) dgemm_go<2>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+  else if (mt <= 4) dgemm_go<4>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+  else if (mt <= 8) dgemm_go<8>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+  else dgemm_go<16>(X, W, out, M, N, K, S, ldo, epi, rs, s);
 }
 
 }  // namespace ms

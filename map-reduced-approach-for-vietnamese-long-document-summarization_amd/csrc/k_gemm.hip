@@ -15,7 +15,9 @@
 // multiplied.  Block order: group-M raster + bijective XCD remap (T1) so that the
 // blocks sharing an A panel run on one XCD's L2.
 // Epilogues fuse the residual add (O, down) and SwiGLU (gate/up rows interleaved
-// per 16 on upload) so no extra HBM pass is spent on them.
+// per 16 on upload) so no extra HBM pass is spent on them; the normalised projections (QKV,
+// gate/up, logits) scale each output row by its deferred RMSNorm factor (kernels.h RowScale,
+// one tile: rs_rinv(ssq[row])).
 #include "kernels.h"
 
 namespace ms {
@@ -33,8 +35,9 @@ template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__ A,
                                                      const bf16_t* __restrict__ W,
                                                      void* __restrict__ out, int M, int N, int K,
-                                                     int ldo) {
+                                                     int ldo, RowScale rs) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GBM * GBK * 2];  // 64 KiB
+  __shared__ float rinv_s[GBM];  // the tile rows' sums of squares (deferred-norm statistics)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
@@ -75,6 +78,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / GBK;
+  // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
+  // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
+  if (rs.ssq && wave < GBM / 64)
+    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(m0 + wave * 64 + lane, M - 1)),
+                                     (LDS_AS void*)(rinv_s + wave * 64), 4, 0, 0);
   stage(0, 0);
   wait_vmcnt0();
   __syncthreads();
@@ -142,13 +150,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
     for (int j = 0; j < 4; ++j) {
       const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
       if (row >= M) continue;
+      const float rv = rs.ssq ? rs_rinv(rinv_s[wm * 64 + m * 16 + fg * 4 + j], rs) : 1.0f;
       if constexpr (EPI == 2) {  // SwiGLU: n even = gate, n odd = up of the same 16 features
 #pragma unroll
         for (int n = 0; n < 4; n += 2) {
           const int col = n0 + wn * 64 + n * 16;  // multiple of 32
           if (col >= N) continue;
           const int f = (col >> 5) * 16 + fr;
-          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[m][n][j], acc[m][n + 1][j]));
+          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[m][n][j] * rv, acc[m][n + 1][j] * rv));
         }
       } else {
 #pragma unroll
@@ -156,9 +165,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
           const int col = n0 + wn * 64 + n * 16 + fr;
           if (col >= N) continue;
           const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[m][n][j]);
+          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[m][n][j] * rv);
           else if constexpr (EPI == 1) ((float*)out)[o] += acc[m][n][j];
-          else ((float*)out)[o] = acc[m][n][j];
+          else ((float*)out)[o] = acc[m][n][j] * rv;
         }
       }
     }
@@ -196,8 +205,9 @@ template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A,
                                                         const bf16_t* __restrict__ W,
                                                         void* __restrict__ out, int M, int N, int K,
-                                                        int ldo) {
+                                                        int ldo, RowScale rs) {
   __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
+  __shared__ float rinv_s[TBM];  // the tile rows' sums of squares (deferred-norm statistics)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (N + TBN - 1) / TBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
@@ -281,6 +291,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   };
 
   const int nk = K / TBK;
+  // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
+  // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
+  if (rs.ssq && wave < TBM / 64)
+    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(m0 + wave * 64 + lane, M - 1)),
+                                     (LDS_AS void*)(rinv_s + wave * 64), 4, 0, 0);
   // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
   stage(0, 0, 0);
   stage(0, 3, 0);
@@ -366,13 +381,14 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
     for (int j = 0; j < 4; ++j) {
       const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
       if (row >= M) continue;
+      const float rv = rs.ssq ? rs_rinv(rinv_s[wr * 128 + mi * 16 + fg * 4 + j], rs) : 1.0f;
       if constexpr (EPI == 2) {  // SwiGLU: ni even = gate, ni odd = up of the same 16 features
 #pragma unroll
         for (int ni = 0; ni < 4; ni += 2) {
           const int col = n0 + wc * 64 + ni * 16;  // multiple of 32
           if (col >= N) continue;
           const int f = (col >> 5) * 16 + fr;
-          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[mi][ni][j], acc[mi][ni + 1][j]));
+          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
         }
       } else {
 #pragma unroll
@@ -380,9 +396,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
           const int col = n0 + wc * 64 + ni * 16 + fr;
           if (col >= N) continue;
           const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[mi][ni][j]);
+          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[mi][ni][j] * rv);
           else if constexpr (EPI == 1) ((float*)out)[o] += acc[mi][ni][j];
-          else ((float*)out)[o] = acc[mi][ni][j];
+          else ((float*)out)[o] = acc[mi][ni][j] * rv;
         }
       }
     }
@@ -394,25 +410,30 @@ static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,
-                 hipStream_t s) {
+                 hipStream_t s, const RowScale* rs_in) {
   if (M <= 0) return;
+  RowScale rs{};
+  if (rs_in && rs_in->ssq && epi != 1) {
+    if (rs_in->tiles != 1) return;  // callers pass one-tile statistics (a norm kernel's)
+    rs = *rs_in;
+  }
   const bool big = g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
   if (big) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {
-      case 0: MS_LAUNCH(gemm256_kernel<0>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
-      case 1: MS_LAUNCH(gemm256_kernel<1>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
-      case 2: MS_LAUNCH(gemm256_kernel<2>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
-      default: MS_LAUNCH(gemm256_kernel<3>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo); break;
+      case 0: MS_LAUNCH(gemm256_kernel<0>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
+      case 1: MS_LAUNCH(gemm256_kernel<1>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
+      case 2: MS_LAUNCH(gemm256_kernel<2>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
+      default: MS_LAUNCH(gemm256_kernel<3>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
     }
     return;
   }
   const int grid = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   switch (epi) {
-    case 0: MS_LAUNCH(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    case 1: MS_LAUNCH(gemm_kernel<1>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    case 2: MS_LAUNCH(gemm_kernel<2>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
-    default: MS_LAUNCH(gemm_kernel<3>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo); break;
+    case 0: MS_LAUNCH(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
+    case 1: MS_LAUNCH(gemm_kernel<1>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
+    case 2: MS_LAUNCH(gemm_kernel<2>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
+    default: MS_LAUNCH(gemm_kernel<3>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
   }
 }
 

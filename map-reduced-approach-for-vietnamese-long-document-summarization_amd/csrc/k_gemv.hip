@@ -14,8 +14,12 @@
 //    both operands use the same permuted k order (lane group g holds k0+16g..+15),
 //    which leaves every dot product unchanged.
 // Fusions that remove whole launches from the decode step:
-//  * (RMSNorm stays a separate launch: recomputing it in each of the hundreds of blocks
-//    of a launch measured slower -- GU 19 -> 35 us, lm_head 142 -> 355 us at M = 8);
+//  * the deferred RMSNorm (kernels.h RowScale): X is already bf16(x * g), written by the
+//    producer of x (RESID_SSQ epilogue or a norm kernel) with per-tile sums of x^2; the block
+//    loads its rows' partial sums ahead of everything else and scales its output rows by
+//    rinv in the epilogue -- no norm launch between the residual update and the projection
+//    (recomputing the norm from the fp32 residual in each block measured slower: every block
+//    re-read x before its weight stream, GU 19 -> 27 us, profiles/r03/v1_norm_fused_ab.txt);
 //  * EPI_ROPE_KV (QKV): Q/K rows are uploaded rope-permuted (dims i and i+64 in one
 //    16-row tile), so the epilogue applies RoPE, writes Q for attention and scatters
 //    K/V into the paged cache;
@@ -56,12 +60,15 @@ size_t gemv_workspace_bytes(int, int, int) { return 256; }
 
 constexpr size_t kMaxLds = 160 * 1024;
 
-// staged X: the M real rows, row stride 2K+16 bytes (the 16-B skew puts the 16 rows of a
-// fragment read on different banks); rows >= M alias row M-1 and are never stored.
-static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
-  size_t xs = xlds ? gemv_x_lds_bytes(M, K) + 64 : 0;  // + kXNorm's per-row 1/rms
+// LDS: the X image (gemv_x_lds_bytes, when staged) or the per-wave partials, whichever is
+// larger, then the deferred-norm factors (gemv_lds_total)
+static size_t gemv_lds_main(const GemvPlan& p, int M, int K, bool xlds) {
+  size_t xs = xlds ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;  // per-wave partials
   return xs > red ? xs : red;
+}
+static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds, const RowScale& rs = RowScale{}) {
+  return gemv_lds_total(gemv_lds_main(p, M, K, xlds), rs, M);
 }
 
 // Split-K (gridDim.y = S > 1, STORE_F32 only): block (x, y) covers k in [y*K, (y+1)*K) of
@@ -73,12 +80,14 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds) {
 //   kXRegs:   each wave loads its OWN k-slice of X (the only part it multiplies) straight
 //             into registers ahead of its weight loads -- no LDS image, no block barrier,
 //             every wave starts its MFMAs as soon as its own bytes have landed.
-// kXNorm: two 1024-thread blocks per CU (<= 64 VGPRs), as the plain gate/up GEMV gets
+// rinv_off: LDS byte offset of the deferred-norm factors (gemv_rinv_offset).
+// Plans of <= 6 register stages (gate/up: U = 3, NT = 2 on 512 blocks) are held to 64 VGPRs so
+// two 1024-thread blocks share a CU (launch bounds: 8 waves per SIMD).
 template <int MT, int NT, int EPI, int U, int XM>
-__global__ __launch_bounds__(1024, (XM == kXNorm && U <= 4) ? 8 : 1) void gemv_kernel(const bf16_t* __restrict__ X,
+__global__ __launch_bounds__(1024, (MT == 1 && U * NT <= 6) ? 8 : 1) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
-                                                    int ldk, int ldo, GemvArgs ga) {
+                                                    int ldk, int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
@@ -92,11 +101,10 @@ __global__ __launch_bounds__(1024, (XM == kXNorm && U <= 4) ? 8 : 1) void gemv_k
     out = (float*)out + (size_t)blockIdx.y * M * ldo;
   }
 
-  // 1. X first (LDS DMA of the block's rows, this wave's slice into registers, or the
-  // RMSNorm of the fp32 residual built in LDS), then this wave's whole W stream: vmcnt
-  // retires in issue order
+  // 0. the output rows' deferred-norm partial sums, 1. X (LDS DMA of the block's rows or this
+  // wave's slice into registers), then this wave's whole W stream: vmcnt retires in issue order
+  rs_dma(smem, rinv_off, ga.rs, M);
   if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
-  if constexpr (XM == kXNorm) gemv_norm_x(smem, ga, M, K, blockIdx.y * K);
   uint4 xr[XM == kXRegs ? U : 1][XM == kXRegs ? MT : 1][2];
   if constexpr (XM == kXRegs) {
 #pragma unroll
@@ -141,7 +149,7 @@ __global__ __launch_bounds__(1024, (XM == kXNorm && U <= 4) ? 8 : 1) void gemv_k
       if constexpr (XM == kXRegs) {
         x0 = as_bf16x8(xr[u][m][0]);
         x1 = as_bf16x8(xr[u][m][1]);
-      } else if constexpr (XM == kXLds || XM == kXNorm) {
+      } else if constexpr (XM == kXLds) {
         const int k0 = kbeg + u * 64 + 16 * fg;
         x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
         x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
@@ -157,7 +165,7 @@ __global__ __launch_bounds__(1024, (XM == kXNorm && U <= 4) ? 8 : 1) void gemv_k
       }
     }
   }
-  gemv_finish<MT, NT, EPI>(acc, smem, M, N, ldo, out, n0, ga);
+  gemv_finish<MT, NT, EPI>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
 }
 
 template <int MT, int NT, int EPI, int U>
@@ -165,29 +173,23 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
                     int S, int ldo, const GemvPlan& p, size_t lds, int xm, const GemvArgs& ga,
                     hipStream_t s) {
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
+  const int ro = (int)gemv_rinv_offset(gemv_lds_main(p, M, K, xm == kXLds));
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
   } else {
     if constexpr (MT * U <= kXRegsMaxFrags) {
       if (xm == kXRegs) {
         MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXRegs>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                  ldo, ga);
-        return;
-      }
-    }
-    if constexpr (MT == 1) {
-      if (xm == kXNorm) {
-        MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXNorm>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                  ldo, ga);
+                  ldo, ro, ga);
         return;
       }
     }
     if (xm == kXLds)
       MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXLds>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                ldo, ga);
+                ldo, ro, ga);
     else
       MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXGlobal>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                ldo, ga);
+                ldo, ro, ga);
   }
 }
 
@@ -236,16 +238,6 @@ bool gemv_supported(int M, int N, int K, int epi) {
   return gemv_lds_bytes(p, M, K, false) <= kMaxLds;
 }
 
-// the kXNorm prologue's limits (gemv_norm_x): one 16-row MFMA tile of X rows, the block's
-// x slice in <= kNormChunks float4 per thread, <= 256 producer tiles, the image in LDS
-bool gemv_norm_supported(int M, int N, int K, int epi, int ssq_tiles, int rt) {
-  if (M < 1 || M > 16 || K % 64 || ssq_tiles < 1 || ssq_tiles > 256) return false;
-  if (epi == MS_GEMV_EPI_ROPE_KV || epi == MS_GEMV_EPI_ARGMAX) return false;
-  const GemvPlan p = gemv_plan(M, N, K, epi, 0, rt);
-  if (p.waves == 0) return false;
-  return gemv_lds_bytes(p, M, K, true) <= kMaxLds;
-}
-
 static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
                           int S, int ldo, int epi, const GemvArgs* ga_in, int force_waves,
                           hipStream_t s) {
@@ -256,14 +248,11 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
   int xm = xl ? kXLds : kXGlobal;
   if (gemv_x_regs() && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
-  if (ga_in && ga_in->xres) {
-    if (!gemv_norm_supported(M, N, K, epi, ga_in->ssq_tiles, rt)) return;  // callers check
-    xm = kXNorm;
-  }
-  const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds || xm == kXNorm);
-  if (lds > kMaxLds) return;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
+  if (epi == MS_GEMV_EPI_ARGMAX) ga.rs = RowScale{};  // r > 0 keeps every row's order
+  const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds, ga.rs);
+  if (lds > kMaxLds) return;
   switch (p.MT) {
     case 1: gemv_go_mt<1>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
     case 2: gemv_go_mt<2>(X, W, out, M, N, K, ldk, S, ldo, epi, p, lds, xm, ga, s); break;
@@ -291,157 +280,6 @@ bool gemv_split_supported(int M, int N, int K, int S) {
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga) {
   gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, ga, force_waves, s);
-}
-
-// ---------------------------------------------------------------- persistent decode GEMV
-// One block per CU for the whole launch.  Block b owns ONE K slice (split s = b % S, K = the
-// slice length) and walks the 16*NT-row tiles t = b / S, + G/S, ... of N: its X slice is
-// staged in LDS ONCE (DMA of the bf16 rows, or built as bf16(rmsnorm(x) * gamma) by the
-// kXNorm prologue), and while a tile is multiplied, reduced across the waves and written, the
-// next tile's weights are already in flight (two register stages).  Compared with one block
-// per tile (gemv_kernel), the per-block X staging, ramp and tail are paid once per CU instead
-// of once per tile, and a CU's weight stream never stops between its tiles.  Results are
-// identical to gemv_kernel's for the same (N, K, S): a tile's summation order is the same
-// (wave slices of U steps, LDS reduction in wave order).
-template <int NT, int EPI, int U, int XM>
-__global__ __launch_bounds__(1024) void pgemv_kernel(const bf16_t* __restrict__ X,
-                                                     const bf16_t* __restrict__ W,
-                                                     void* __restrict__ out, int M, int N, int K,
-                                                     int ldk, int ldo, int S, GemvArgs ga) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int ELEMS = NT * 256;  // floats of one wave's tile result
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const int fr = lane & 15, fg = lane >> 4;
-  const int split = blockIdx.x % S, per = gridDim.x / S;
-  const int rows = 16 * NT, ntiles = (N + rows - 1) / rows;
-  const int kbeg = wave * U * 64;
-  float* red0 = (float*)(smem + gemv_x_lds_bytes(M, K) + 64);
-  float* red1 = red0 + nw * ELEMS;
-  if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
-    X += (size_t)split * K;
-    W += (size_t)split * K;
-    out = (float*)out + (size_t)split * M * ldo;
-  }
-  if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
-  uint4 wa[U][NT][2], wb[U][NT][2];
-  auto load = [&](uint4 (&w)[U][NT][2], int t) {
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const bf16_t* wp = W + (size_t)min(t * rows + n * 16 + fr, N - 1) * ldk + kbeg + 16 * fg;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        w[u][n][0] = ldw16(wp + u * 64);
-        w[u][n][1] = ldw16(wp + u * 64 + 8);
-      }
-    }
-  };
-  auto tile = [&](const uint4 (&w)[U][NT][2], int t, float* red) {
-    f32x4 acc[NT];
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int xrow = min(fr, M - 1);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int k0 = kbeg + u * 64 + 16 * fg;
-      const bf16x8 x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
-      const bf16x8 x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
-#pragma unroll
-      for (int n = 0; n < NT; ++n) {
-        acc[n] = mfma16(x0, as_bf16x8(w[u][n][0]), acc[n]);
-        acc[n] = mfma16(x1, as_bf16x8(w[u][n][1]), acc[n]);
-      }
-    }
-#pragma unroll
-    for (int n = 0; n < NT; ++n) *(f32x4*)&red[wave * ELEMS + (n * 64 + lane) * 4] = acc[n];
-    lds_sync();  // LDS only: the next tile's weights stay in flight
-    gemv_epilogue<1, NT, EPI>(red, M, N, ldo, out, t * rows, ga);
-  };
-  int t = blockIdx.x / S;
-  if (t < ntiles) load(wa, t);
-  __builtin_amdgcn_sched_barrier(0);
-  if constexpr (XM == kXNorm) gemv_norm_x(smem, ga, M, K, split * K);
-  if constexpr (XM == kXLds) {
-    // the X image landed once at most this block's first weight loads are pending
-    if (t < ntiles) __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
-    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-    __builtin_amdgcn_s_barrier();
-  }
-  while (t < ntiles) {
-    const int t1 = t + per;
-    if (t1 < ntiles) load(wb, t1);
-    __builtin_amdgcn_sched_barrier(0);
-    tile(wa, t, red0);
-    t = t1;
-    if (t >= ntiles) break;
-    const int t2 = t + per;
-    if (t2 < ntiles) load(wa, t2);
-    __builtin_amdgcn_sched_barrier(0);
-    tile(wb, t, red1);
-    t = t2;
-  }
-}
-
-struct PgemvPlan {
-  int waves, U, grid;
-};
-// waves <= 16 splitting the slice's 64-wide steps evenly with U <= 4 (two register stages of
-// U*NT*2 uint4 per lane), grid = one block per CU rounded down to a multiple of S
-static PgemvPlan pgemv_plan(int N, int Ks, int S, int NT) {
-  PgemvPlan p{0, 0, 0};
-  const int steps = Ks / 64;
-  for (int w = 16; w >= 4; --w)
-    if (steps % w == 0 && steps / w <= 4 && (steps / w) * NT <= 6) { p.waves = w; p.U = steps / w; break; }
-  p.grid = (256 / S) * S;
-  return p;
-}
-
-static size_t pgemv_lds_bytes(const PgemvPlan& p, int M, int Ks, int NT) {
-  return gemv_x_lds_bytes(M, Ks) + 64 + 2 * (size_t)p.waves * NT * 256 * 4;
-}
-
-bool pgemv_supported(int M, int N, int K, int S, int epi, bool norm) {
-  if (M < 1 || M > 16 || S < 1 || K % S || (K / S) % 64) return false;
-  if (epi != MS_GEMV_EPI_STORE_F32 && epi != MS_GEMV_EPI_SWIGLU) return false;
-  if (S > 1 && epi != MS_GEMV_EPI_STORE_F32) return false;
-  const int NT = epi == MS_GEMV_EPI_SWIGLU ? 2 : 1;
-  if (N % (16 * NT)) return false;
-  const PgemvPlan p = pgemv_plan(N, K / S, S, NT);
-  if (p.waves == 0 || p.grid < S) return false;
-  (void)norm;
-  return pgemv_lds_bytes(p, M, K / S, NT) <= kMaxLds;
-}
-
-template <int NT, int EPI, int XM>
-static void pgemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int Ks, int ldk, int ldo,
-                     int S, const PgemvPlan& p, const GemvArgs& ga, hipStream_t s) {
-  const size_t lds = pgemv_lds_bytes(p, M, Ks, NT);
-#define PG(U_) MS_LAUNCH((pgemv_kernel<NT, EPI, U_, XM>), dim3(p.grid), dim3(64 * p.waves), lds, s, X, W, out, M, \
-                         N, Ks, ldk, ldo, S, ga)
-  switch (p.U) {
-    case 1: PG(1); break;
-    case 2: PG(2); break;
-    case 3: PG(3); break;
-    default: PG(4); break;
-  }
-#undef PG
-}
-
-void launch_pgemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  const GemvArgs* ga_in, hipStream_t s) {
-  if (!pgemv_supported(M, N, K, S, epi, ga_in && ga_in->xres)) return;  // callers check
-  const int NT = epi == MS_GEMV_EPI_SWIGLU ? 2 : 1;
-  const int Ks = K / S;
-  const PgemvPlan p = pgemv_plan(N, Ks, S, NT);
-  GemvArgs ga{};
-  if (ga_in) ga = *ga_in;
-  const bool norm = ga.xres != nullptr;
-  if (epi == MS_GEMV_EPI_SWIGLU) {
-    if (norm) pgemv_go<2, MS_GEMV_EPI_SWIGLU, kXNorm>(X, W, out, M, N, Ks, K, ldo, S, p, ga, s);
-    else pgemv_go<2, MS_GEMV_EPI_SWIGLU, kXLds>(X, W, out, M, N, Ks, K, ldo, S, p, ga, s);
-  } else {
-    if (norm) pgemv_go<1, MS_GEMV_EPI_STORE_F32, kXNorm>(X, W, out, M, N, Ks, K, N, S, p, ga, s);
-    else pgemv_go<1, MS_GEMV_EPI_STORE_F32, kXLds>(X, W, out, M, N, Ks, K, N, S, p, ga, s);
-  }
 }
 
 // ---------------------------------------------------------------- argmax of partials

@@ -12,16 +12,12 @@ thread_local ProfEvents* g_prof = nullptr;
 
 // ---------------------------------------------------------------- embedding
 // x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores
-// ssq (optional): ssq[t] = sum of x[t][:]^2 (fixed order: per thread, then the wave tree, then
-// the 4 waves in order) -- the one-tile RMSNorm statistics a kXNorm GEMV prologue consumes
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
                                                     const bf16_t* __restrict__ emb, int H,
-                                                    float* __restrict__ x, float* __restrict__ ssq) {
-  __shared__ float red[4];
+                                                    float* __restrict__ x) {
   const int t = blockIdx.x;
   const bf16_t* row = emb + (size_t)ids[t] * H;
   float* xo = x + (size_t)t * H;
-  float ss = 0.f;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     uint4 v = *(const uint4*)(row + c * 8);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -32,13 +28,7 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
     b.z = __uint_as_float(w[3] << 16); b.w = __uint_as_float(w[3] & 0xFFFF0000u);
     *(float4*)(xo + c * 8) = a;
     *(float4*)(xo + c * 8 + 4) = b;
-    ss += ((a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w)) + ((b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w));
   }
-  if (!ssq) return;  // block-uniform
-  ss = wave_sum(ss);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-  __syncthreads();
-  if (threadIdx.x == 0) ssq[t] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 // Chained decode steps (engine.cpp decode_run): the step's argmax ids become the next
@@ -69,19 +59,20 @@ void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring,
   MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
 }
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
-                  float* ssq) {
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
   if (T <= 0) return;
-  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x, ssq);
+  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
 }
 
 // ---------------------------------------------------------------- RMSNorm
-// y = bf16( (x * rsqrt(mean(x^2) + eps)) * w ), one 256-thread block per row; the row is
-// read once (<= 8 float4 per thread kept in registers, H <= 8192).
+// The GEMM input of a normalised projection (deferred RMSNorm, kernels.h RowScale):
+// y = bf16(x * w) and ssq[r] = sum of x^2 (per thread, the wave tree, then the 4 waves in
+// order), one 256-thread block per row; the row is read once (<= 8 float4 per thread kept in
+// registers, H <= 8192).  The projection scales its output rows by rs_rinv(ssq[r]).
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x,
                                                       const bf16_t* __restrict__ w,
-                                                      bf16_t* __restrict__ y, int H, float eps,
-                                                      const int32_t* __restrict__ row_idx) {
+                                                      bf16_t* __restrict__ y, float* __restrict__ ssq,
+                                                      int H, const int32_t* __restrict__ row_idx) {
   __shared__ float red[4];
   const int r = blockIdx.x;
   const int src = row_idx ? row_idx[r] : r;
@@ -95,11 +86,6 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
     v[k] = *(const float4*)(xr + c * 4);
     if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
   }
-  ss = wave_sum(ss);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-  __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
-  const float rinv = 1.0f / sqrtf(tot / (float)H + eps);
   bf16_t* yr = y + (size_t)r * H;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -109,20 +95,25 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
     float g0 = __uint_as_float(wv.x << 16), g1 = __uint_as_float(wv.x & 0xFFFF0000u);
     float g2 = __uint_as_float(wv.y << 16), g3 = __uint_as_float(wv.y & 0xFFFF0000u);
     uint2 o;
-    o.x = pack2bf((v[k].x * rinv) * g0, (v[k].y * rinv) * g1);
-    o.y = pack2bf((v[k].z * rinv) * g2, (v[k].w * rinv) * g3);
+    o.x = pack2bf(v[k].x * g0, v[k].y * g1);
+    o.y = pack2bf(v[k].z * g2, v[k].w * g3);
     *(uint2*)(yr + c * 4) = o;
   }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssq[r] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
+void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, float* ssq, int rows, int H,
                     const int32_t* row_idx, hipStream_t s) {
   if (rows <= 0) return;
-  MS_LAUNCH(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, H, eps, row_idx);
+  MS_LAUNCH(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, ssq, H, row_idx);
 }
 
-// Decode: the residual update of a split-K projection fused with the next RMSNorm.
-// x[r] += (slab_0[r] + slab_1[r] + ... + slab_{S-1}[r]), then y[r] = bf16((x[r]*rinv)*w).
+// Decode: the residual update of a split-K projection fused with the next norm's input.
+// x[r] += (slab_0[r] + slab_1[r] + ... + slab_{S-1}[r]), then y[r] = bf16(x[r] * w) and
+// ssq[r] = sum of x[r]^2 (rmsnorm_kernel's order): the next projection's deferred RowScale.
 // The summation order is fixed (slab order), so the result does not depend on timing or on
 // the other rows.  One block per row; every load (x, w, all S slabs) is issued before the
 // first add (S is a template parameter: a runtime trip count serialises the loads).
@@ -131,8 +122,8 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
                                                                const float* __restrict__ slabs,
                                                                int rows,
                                                                const bf16_t* __restrict__ w,
-                                                               bf16_t* __restrict__ y, int H,
-                                                               float eps) {
+                                                               bf16_t* __restrict__ y,
+                                                               float* __restrict__ ssq, int H) {
   constexpr int KMAX = 3;  // float4 per thread: H <= 3072
   __shared__ float red[4];
   const int r = blockIdx.x;
@@ -176,11 +167,6 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
-  ss = wave_sum(ss);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-  __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
-  const float rinv = 1.0f / sqrtf(tot / (float)H + eps);
   bf16_t* yr = y + (size_t)r * H;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
@@ -190,24 +176,28 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
     const float g0 = __uint_as_float(wv[k].x << 16), g1 = __uint_as_float(wv[k].x & 0xFFFF0000u);
     const float g2 = __uint_as_float(wv[k].y << 16), g3 = __uint_as_float(wv[k].y & 0xFFFF0000u);
     uint2 o;
-    o.x = pack2bf((v[k].x * rinv) * g0, (v[k].y * rinv) * g1);
-    o.y = pack2bf((v[k].z * rinv) * g2, (v[k].w * rinv) * g3);
+    o.x = pack2bf(v[k].x * g0, v[k].y * g1);
+    o.y = pack2bf(v[k].z * g2, v[k].w * g3);
     *(uint2*)(yr + c * 4) = o;
   }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssq[r] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 bool residual_rmsnorm_supported(int S, int H) { return S >= 0 && S <= 8 && H % 4 == 0 && H <= 3072; }
 
 void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
-                             int rows, int H, float eps, hipStream_t s) {
+                             float* ssq, int rows, int H, hipStream_t s) {
   if (rows <= 0) return;
   if (H > 3072) {  // wider models: the plain kernel (S = 0 only)
-    launch_rmsnorm(x, w, y, rows, H, eps, nullptr, s);
+    launch_rmsnorm(x, w, y, ssq, rows, H, nullptr, s);
     return;
   }
 #define RN(S_)                                                                                 \
   case S_:                                                                                     \
-    MS_LAUNCH(residual_rmsnorm_kernel<S_>, dim3(rows), dim3(256), 0, s, x, slabs, rows, w, y, H, eps); \
+    MS_LAUNCH(residual_rmsnorm_kernel<S_>, dim3(rows), dim3(256), 0, s, x, slabs, rows, w, y, ssq, H); \
     break;
   switch (S) { RN(0) RN(1) RN(2) RN(3) RN(4) RN(5) RN(6) RN(7) RN(8) }
 #undef RN

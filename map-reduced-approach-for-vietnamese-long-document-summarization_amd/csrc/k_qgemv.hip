@@ -187,8 +187,9 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 template <int MT, int NT, int EPI, int SBW, int XM>
 __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
-                                                     int ldo, GemvArgs ga) {
+                                                     int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  rs_dma(smem, rinv_off, ga.rs, M);  // the output rows' deferred-norm sums, ahead of every load
   // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
   // of the full row, where K is the per-split length; X and out shift to that slab.
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
@@ -347,7 +348,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         }
       }
   }
-  gemv_finish<MT, NT, EPI>(acc, smem, M, N, ldo, out, n0, ga);
+  gemv_finish<MT, NT, EPI>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
 }
 
 struct QPlan {
@@ -376,11 +377,14 @@ static bool qx_in_lds(int M, int K) {
 
 static bool qx_in_regs(const QPlan& p) { return qgemv_x_regs() && p.MT * p.SBW == 1; }
 
-static size_t qlds(const QPlan& p, int M, int K) {
+static size_t qlds_main(const QPlan& p, int M, int K) {
   // X image (when it fits and X is not taken into registers)
   const size_t xs = (!qx_in_regs(p) && qx_in_lds(M, K)) ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
+}
+static size_t qlds(const QPlan& p, int M, int K, const RowScale& rs = RowScale{}) {
+  return gemv_lds_total(qlds_main(p, M, K), rs, M);
 }
 
 bool qgemv_supported(int M, int N, int K, int epi) {
@@ -392,15 +396,18 @@ bool qgemv_supported(int M, int N, int K, int epi) {
 
 template <int MT, int NT, int EPI>
 static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
-                     const QPlan& p, const GemvArgs& ga, hipStream_t s, int S = 1) {
-  const size_t lds = qlds(p, M, K);
+                     const QPlan& p, const GemvArgs& ga_in, hipStream_t s, int S = 1) {
+  GemvArgs ga = ga_in;
+  if (EPI == MS_GEMV_EPI_ARGMAX) ga.rs = RowScale{};  // r > 0 keeps every row's order
+  const size_t lds = qlds(p, M, K, ga.rs);
+  const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;
   } else {
     const bool xl = qx_in_lds(M, K);
 #define QL(SBW_, XM_) \
-    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ga)
+    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ro, ga)
     if (p.SBW == 4 && xl) QL(4, kXLds);
     else if (p.SBW == 4) QL(4, kXGlobal);
     else if (p.SBW == 3 && xl) QL(3, kXLds);
@@ -450,12 +457,13 @@ bool qgemv_split_supported(int M, int N, int K, int S) {
 // fp32 partial slabs [S][M][N] over S equal K ranges (super-block aligned); the caller
 // folds them (residual_rmsnorm_kernel / the decode attention prologue)
 void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
-                        hipStream_t s) {
+                        hipStream_t s, const GemvArgs* ga_in) {
   if (M <= 0) return;
   const int Ks = K / S;
   const QPlan p = qplan(M, N, Ks, MS_GEMV_EPI_STORE_F32);
   if (p.waves == 0) return;  // callers check qgemv_split_supported()
-  const GemvArgs ga{};
+  GemvArgs ga{};
+  if (ga_in) ga = *ga_in;
   switch (p.MT) {
     case 1: qgemv_go<1, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;
     case 2: qgemv_go<2, 1, MS_GEMV_EPI_STORE_F32>(X, q, slabs, M, N, Ks, N, p, ga, s, S); break;

@@ -34,15 +34,32 @@ struct DecodeAttnArgs {
   int32_t ppw;              // pages per wave, fixed per engine (attn_decode_ppw); 0 = 2
 };
 
-// ssq: optional per-row sums of squares [T] (one RMSNorm-statistics tile, see gemv_norm_x)
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
-                  float* ssq = nullptr);
+// The deferred RMSNorm of the numerics contract (oracle/llama_ref.py): a
+// normalised projection (QKV, gate/up, lm_head) multiplies the bf16 GEMM input bf16(x * g) by
+// W and scales output row r by rinv(r) = 1/sqrt(sum_t ssq[t][r] / H + eps), where ssq holds
+// partial sums of x[r]^2 [tiles][rows] written by the producer of x (a norm kernel: one tile;
+// a RESID_SSQ GEMV epilogue: one per column tile).  Every consumer forms the sum in the same
+// order (tile t = lane + 64 i added in i order per lane, then the wave's xor tree; with one
+// tile that is ssq[0][r] exactly), so a row's factor depends only on (tiles, H) -- never on
+// the number of rows or on the kernel.  ssq == nullptr: no scale.
+struct RowScale {
+  const float* ssq;
+  int tiles, H;
+  float eps;
+};
+__host__ __device__ __forceinline__ float rs_rinv(float sum, const RowScale& rs) {
+  return 1.0f / sqrtf(sum / (float)rs.H + rs.eps);
+}
+
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
 // chained decode: next ids <- this step's argmax (clamped into [0, V)), positions and key
 // counts += 1 in the step-argument blob [ids | positions | slots | key counts | step], and the
 // raw ids appended to ring row `step` (B <= 256)
 void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring, int B, int V,
                            hipStream_t s);
-void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, int rows, int H, float eps,
+// the GEMM input of a normalised projection: y[r] = bf16(x[row_idx[r]] * w), ssq[r] = sum of
+// x[row_idx[r]]^2 (one-tile RowScale); row_idx optional (gather)
+void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, float* ssq, int rows, int H,
                     const int32_t* row_idx, hipStream_t s);
 // RoPE on Q (in place, rope-permuted -> natural dim order) and K; K,V scattered into the
 // paged cache.  Q/K heads arrive in the rope-permuted row order of the fused weights.
@@ -51,9 +68,10 @@ void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     KVView kv, hipStream_t s);
 void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s);
 
-// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0
+// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0; rs (one tile, or null):
+// the deferred RMSNorm scale of the output rows (epilogues 0, 2, 3)
 void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
-                 int epi, hipStream_t s);
+                 int epi, hipStream_t s, const RowScale* rs = nullptr);
 // tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
 void set_gemm_variant(int v);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
@@ -67,9 +85,10 @@ enum {
   // greedy argmax partials: out = {max, id} float2 [M][tiles] of each 16-column tile
   // (ties -> lowest id, NaN never wins); launch_argmax_partials finishes the rows
   MS_GEMV_EPI_ARGMAX = 5,
-  // residual update + RMSNorm statistics (decode O / down, no split-K): out = x fp32 [M][ldo],
-  // x[r][c] += acc, and ga.ssq_out[tile][r] = sum over the tile's columns of the new x[r][c]^2
-  // (a fixed lane tree): the next GEMV's kXNorm prologue finishes the RMSNorm from them
+  // residual update + the next RMSNorm's inputs (decode O / down, no split-K): out = x fp32
+  // [M][ldo], x[r][c] += acc; ga.ssq_out[tile][r] = sum over the tile's columns of the new
+  // x[r][c]^2 (a fixed lane tree) and ga.xg_out[r][c] = bf16(x[r][c] * ga.gamma[c]): the next
+  // projection's GEMM input and its deferred row scale (RowScale), with no norm launch
   MS_GEMV_EPI_RESID_SSQ = 6
 };
 struct GemvArgs {
@@ -83,40 +102,32 @@ struct GemvArgs {
   // weight rows per tile (NT = 1 plans; 0 = 16): 12 puts the 3072-row O / down projections on
   // exactly 256 workgroups (one per CU) without split-K
   int rt;
-  // RESID_SSQ epilogue: per-tile sums of squares [tiles][M]
+  // RESID_SSQ epilogue: per-tile sums of squares [tiles][M], the next norm's gain [ldo] and
+  // the bf16 GEMM input it feeds [M][ldo]
   float* ssq_out;
-  // RMSNorm prologue (X = bf16(rmsnorm(xres) * gamma) built in LDS, no separate norm launch):
-  // xres fp32 [M][hdim], ssq_in [ssq_tiles][M] from the RESID_SSQ producer, gamma bf16 [hdim]
-  const float* xres;
-  const float* ssq_in;
   const bf16_t* gamma;
-  int ssq_tiles, hdim;
-  float eps;
+  bf16_t* xg_out;
+  // deferred RMSNorm scale of the output rows (STORE_BF16 / STORE_F32 / SWIGLU / ROPE_KV /
+  // ARGMAX epilogues)
+  RowScale rs;
 };
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
-// consumer adds them in slab order (launch_residual_rmsnorm)
+// consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)
 bool gemv_split_supported(int M, int N, int K, int S);
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga = nullptr);
-// persistent decode GEMV (one block per CU walking its tiles, next tile's weights in flight):
-// STORE_F32 split-K slabs [S][M][N] (ldo = N) or SWIGLU (S = 1); ga->xres set = kXNorm prologue
-bool pgemv_supported(int M, int N, int K, int S, int epi, bool norm);
-void launch_pgemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  const GemvArgs* ga, hipStream_t s);
-// whether a GEMV (plain or one split of a split-K launch, K = its slice) can build its X as
-// the RMSNorm of the fp32 residual itself (GemvArgs.xres/ssq_in/gamma: the kXNorm prologue)
-bool gemv_norm_supported(int M, int N, int K, int epi, int ssq_tiles, int rt);
 // X [M][ldk] and W [N][ldk] rows of stride ldk >= K (tuning hook: padded weight layouts)
 void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
                          int ldo, int epi, hipStream_t s);
 // rows of {max, id} partials [rows][tiles] -> ids (-1: no finite maximum)
 void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* out, hipStream_t s);
 
-// x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = RMSNorm(x)*w.
-// S = 0: plain RMSNorm.  Supported: S <= 8, H <= 3072 (H > 3072 only with S = 0).
+// x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = bf16(x * w)
+// and ssq[r] = sum of x[r]^2 (the one-tile RowScale of the projection y feeds).  S = 0: no
+// slabs.  Supported: S <= 8, H <= 3072 (H > 3072 only with S = 0).
 bool residual_rmsnorm_supported(int S, int H);
 void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
-                             int rows, int H, float eps, hipStream_t s);
+                             float* ssq, int rows, int H, hipStream_t s);
 size_t gemv_workspace_bytes(int M, int N, int K);
 bool gemv_supported(int M, int N, int K, int epi);
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
@@ -130,7 +141,7 @@ void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
 // the GEMV's except ROPE_KV; N % 64 == 0, K % (64 S) == 0.
 bool dgemm_supported(int M, int N, int K, int S, int epi);
 void launch_dgemm(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  hipStream_t s);
+                  hipStream_t s, const RowScale* rs = nullptr);
 
 // ---- ggml K-quant weights (k_qgemv.hip)
 enum { MS_QT_Q4_K = 12, MS_QT_Q6_K = 14 };  // ggml_type ids
@@ -162,7 +173,7 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 bool qgemv_supported(int M, int N, int K, int epi);
 bool qgemv_split_supported(int M, int N, int K, int S);
 void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
-                        hipStream_t s);
+                        hipStream_t s, const GemvArgs* ga = nullptr);
 void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga, hipStream_t s);
 
@@ -171,23 +182,24 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 // decode attention input: either bf16 qkv rows already roped with K/V in the cache
 // (slabs == nullptr), or S fp32 split-K slabs of the QKV projection (rope-permuted Q/K rows):
 // the kernel then adds the slabs, applies RoPE and writes the new token's K/V itself.
+// With slabs, rs is the deferred RMSNorm scale of the QKV rows (tiles <= 256): the kernel
+// rounds q/k/v = bf16(rinv(b) * sum of the slabs).
 struct DecodeQKV {
   const bf16_t* qkv;
   const float* slabs;
   int S;
   const float* cos_tab;
   const float* sin_tab;
+  RowScale rs;
 };
-// workspace must be zero-filled once at allocation (split-combine tickets live there)
+// split partials of decode attention (combined by a second launch)
 size_t attn_decode_workspace_bytes(int B, int Hq, int max_len);
-// the split-combine counters at the start of that workspace (zeroed before each step)
-size_t attn_decode_ticket_bytes();
 bool attn_decode_supported(int B, int Hq, int Hk, int max_len);
 // pages per wave of an engine's decode attention (from its max_batch / max_ctx, never from
 // one step's batch: the split boundaries set a sequence's summation order)
 int attn_decode_ppw(int max_batch, int Hk, int max_ctx);
 void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
-                        DecodeAttnArgs a, float* ws, hipStream_t s, bool fused_combine = false);
+                        DecodeAttnArgs a, float* ws, hipStream_t s);
 
 // synthetic weights (oracle/synth.py restates this generator)
 // row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the

@@ -34,7 +34,7 @@ EXPORTED = (
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
-    "ms_op_pgemv",
+    "ms_op_gemv_resid", "ms_op_set_row_scale",
 )
 
 
@@ -102,7 +102,8 @@ def load() -> C.CDLL:
         "ms_forward_packed": (i32, [vp, pi32, pi32, i32, i32, vp, vp]),
         "ms_set_eos_ids": (i32, [vp, pi32, i32]),
         "ms_op_gemv_strided": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
-        "ms_op_pgemv": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
+        "ms_op_gemv_resid": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]),
+        "ms_op_set_row_scale": (i32, [vp, i32, i32, C.c_float]),
         "ms_submit_forced": (i32, [vp, pi32, i32, pi32, i32, i32, u32, u64]),
         "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_workspace": (i64, [i32, i32, i32]),
@@ -110,8 +111,8 @@ def load() -> C.CDLL:
         "ms_op_gemv_tuned": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp, i32, vp]),
         "ms_op_gemv_split": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_dgemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
-        "ms_op_residual_rmsnorm": (i32, [vp, vp, i32, vp, vp, i32, i32, C.c_float, vp]),
-        "ms_op_rmsnorm": (i32, [vp, vp, vp, i32, i32, C.c_float, vp, vp]),
+        "ms_op_residual_rmsnorm": (i32, [vp, vp, i32, vp, vp, vp, i32, i32, vp]),
+        "ms_op_rmsnorm": (i32, [vp, vp, vp, vp, i32, i32, vp, vp]),
         "ms_set_gemm_variant": (i32, [i32]),
         "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
         "ms_op_argmax_partials": (i32, [vp, i32, i32, vp, vp]),
@@ -119,7 +120,10 @@ def load() -> C.CDLL:
         "ms_quant_manifest": (i32, [vp, pi32, i32]),
         "ms_declare_weight_q": (i32, [vp, i32, i32, i32]),
     }
+    ab = bool(os.environ.get("MAPSUM_LIB"))  # an A/B build may predate the newest op hooks
     for name, (res, args) in sig.items():
+        if ab and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -10,12 +10,15 @@ public Llama-3.2 one (RMSNorm, GQA attention with llama3-scaled rotate-half
 RoPE, SwiGLU MLP, tied lm_head) and is pinned against
 ``transformers.LlamaForCausalLM`` by ``tests/golden/make_golden.py``.
 
-Rounding points (the engine's numerics contract, DESIGN.md §Numerics):
-  residual stream fp32; every GEMM input bf16, fp32 accumulate; RMSNorm output,
-  Q/K/V, RoPE output, attention output and the SwiGLU product rounded to bf16;
-  attention scores/softmax fp32; logits fp32; argmax ties -> lowest id.
-The only deliberate difference from the HIP path: softmax here is exact fp32
-(the flash kernels round P to bf16 before P.V), which the tests' tolerances cover.
+Rounding points (the engine's numerics contract, DESIGN.md §2):
+  residual stream fp32; every GEMM input bf16, fp32 accumulate; a normalised projection
+  (QKV, gate/up, lm_head) multiplies bf16(x * g) by W and scales each output row by the
+  RMSNorm factor r = 1/sqrt(mean(x^2) + eps) in fp32 -- r * (bf16(x*g) . W^T), the
+  deferred form of W . (x*r*g), so the producer of x can emit the GEMM input without
+  knowing the row's norm; Q/K/V, RoPE output, attention output and the SwiGLU product
+  rounded to bf16; attention scores/softmax fp32; logits fp32; argmax ties -> lowest id.
+The only deliberate difference from the HIP path: softmax here is exact fp32 (the flash
+kernels feed P to the P.V MFMAs as hi + lo bf16 halves), which the tests' tolerances cover.
 """
 from __future__ import annotations
 
@@ -52,10 +55,20 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32)
 
 
-def rmsnorm(x: np.ndarray, g: np.ndarray, eps: float, rnd=bf16_rne) -> np.ndarray:
+def rms_rinv(x: np.ndarray, eps: float) -> np.ndarray:
+    """The RMSNorm factor r = 1/sqrt(mean(x^2) + eps) per row, [..., 1] fp32."""
     ms = np.mean(x.astype(np.float32) ** 2, axis=-1, keepdims=True, dtype=np.float32)
-    r = (np.float32(1.0) / np.sqrt(ms + np.float32(eps))).astype(np.float32)
-    return rnd((x * r) * g)
+    return (np.float32(1.0) / np.sqrt(ms + np.float32(eps))).astype(np.float32)
+
+
+def norm_input(x: np.ndarray, g: np.ndarray, rnd=bf16_rne) -> np.ndarray:
+    """The bf16 GEMM input of a normalised projection: bf16(x * g) (r applied after the GEMM)."""
+    return rnd(x * g)
+
+
+def rmsnorm(x: np.ndarray, g: np.ndarray, eps: float, rnd=bf16_rne) -> np.ndarray:
+    """Plain RMSNorm (x * r) * g, rounded: for callers that want the normalised rows."""
+    return rnd((x * rms_rinv(x, eps)) * g)
 
 
 def apply_rope(x: np.ndarray, cos: np.ndarray, sin: np.ndarray, rnd=bf16_rne) -> np.ndarray:
@@ -102,10 +115,10 @@ class OracleLlama:
         x = w["embed"][ids].astype(np.float32)
         probes = []
         for l, L in enumerate(w["layers"]):
-            xn = rmsnorm(x, L["attn_norm"], cfg.norm_eps, rnd)
-            q = rnd(xn @ L["wq"].T).reshape(T, Hq, D)
-            k = rnd(xn @ L["wk"].T).reshape(T, Hk, D)
-            v = rnd(xn @ L["wv"].T).reshape(T, Hk, D)
+            xg, r = norm_input(x, L["attn_norm"], rnd), rms_rinv(x, cfg.norm_eps)
+            q = rnd(r * (xg @ L["wq"].T)).reshape(T, Hq, D)
+            k = rnd(r * (xg @ L["wk"].T)).reshape(T, Hk, D)
+            v = rnd(r * (xg @ L["wv"].T)).reshape(T, Hk, D)
             q = apply_rope(q, cos, sin, rnd)
             k = apply_rope(k, cos, sin, rnd)
             if cache["k"][l] is not None:
@@ -123,17 +136,17 @@ class OracleLlama:
             p = p / p.sum(axis=-1, keepdims=True)
             o = rnd(np.matmul(p.astype(np.float32), vq.transpose(1, 0, 2)).transpose(1, 0, 2))  # [T, Hq, D]
             x = x + o.reshape(T, Hq * D) @ L["wo"].T
-            xn = rmsnorm(x, L["ffn_norm"], cfg.norm_eps, rnd)
-            g = xn @ L["w_gate"].T
-            u = xn @ L["w_up"].T
+            xg, r = norm_input(x, L["ffn_norm"], rnd), rms_rinv(x, cfg.norm_eps)
+            g = r * (xg @ L["w_gate"].T)
+            u = r * (xg @ L["w_up"].T)
             h = rnd(silu(g) * u)
             x = x + h @ L["w_down"].T
             if collect:
                 probes.append(x.copy())
         cache["len"] = p0 + T
         xs = x if all_logits else x[-1:]
-        xn = rmsnorm(xs, w["final_norm"], cfg.norm_eps, rnd)
-        logits = xn @ w["lm_head"].T
+        xg, r = norm_input(xs, w["final_norm"], rnd), rms_rinv(xs, cfg.norm_eps)
+        logits = r * (xg @ w["lm_head"].T)
         return (logits if all_logits else logits[0]), probes
 
     def generate(self, ids, num_predict: int, eos_ids=(), ignore_eos: bool = False):

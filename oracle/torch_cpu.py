@@ -96,8 +96,14 @@ class TorchCpuLlama:
         return torch.cat([a * c - b * s, b * c + a * s], -1).to(self.dt)
 
     def _norm(self, x, w):
+        """The deferred RMSNorm of the numerics contract (oracle/llama_ref.py): the GEMM input
+        bf16(x * w) and the row factor r the projection's output is scaled by."""
         xf = x.float()
-        return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.cfg.norm_eps)).to(self.dt) * w
+        return (xf * w.float()).to(self.dt), torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.cfg.norm_eps)
+
+    def _proj(self, x, w, W):
+        xg, r = self._norm(x, w)
+        return (xg @ W.T).float() * r
 
     @torch.inference_mode()
     def forward(self, ids, cache, p0):
@@ -108,7 +114,7 @@ class TorchCpuLlama:
         pos = torch.arange(p0, p0 + T)
         x = self.embed[ids].float()
         for l, L in enumerate(self.layers):
-            qkv = self._norm(x, L["n1"]) @ L["wqkv"].T
+            qkv = self._proj(x, L["n1"], L["wqkv"]).to(self.dt)
             q = self._rope(qkv[:, :Hq * D].view(T, Hq, D), pos)
             k = self._rope(qkv[:, Hq * D:(Hq + Hk) * D].view(T, Hk, D), pos)
             v = qkv[:, (Hq + Hk) * D:].view(T, Hk, D)
@@ -119,10 +125,10 @@ class TorchCpuLlama:
             o = F.scaled_dot_product_attention(q.transpose(0, 1), K, V, is_causal=(T > 1 and p0 == 0),
                                                scale=1.0 / math.sqrt(D))
             x = x + (o.transpose(0, 1).reshape(T, Hq * D) @ L["wo"].T).float()
-            gu = self._norm(x, L["n2"]) @ L["wgu"].T
+            gu = self._proj(x, L["n2"], L["wgu"])
             h = F.silu(gu[:, :cfg.ffn].float()) * gu[:, cfg.ffn:].float()
             x = x + (h.to(self.dt) @ L["wdown"].T).float()
-        self.last_logits = (self._norm(x[-1:], self.final_norm) @ self.lm_head.T).float()[0]
+        self.last_logits = self._proj(x[-1:], self.final_norm, self.lm_head)[0]
         return int(torch.argmax(self.last_logits))
 
     def new_cache(self, max_ctx):

@@ -207,14 +207,21 @@ def test_gemv_split_slabs_vs_fp64(lib, dev, M, N, K, S):
     assert rel(slabs.double().sum(0).cpu(), Xd @ Wd.T) < 2e-6
 
 
+def _ssq_ref(x):
+    return (x.double() * x.double()).sum(-1)
+
+
 @pytest.mark.parametrize("S", [0, 1, 4])
 def test_residual_rmsnorm(lib, dev, S):
+    """Residual fold + the next normalised projection's input: x += slabs (slab order),
+    y = bf16(x * w), ssq = sum of x^2 -- the deferred RMSNorm."""
     g = torch.Generator(device="cpu").manual_seed(11 + S)
     rows, H = 8, 3072
     x = (torch.randn(rows, H, generator=g) * 3).to(dev)
     slabs = torch.randn(max(S, 1), rows, H, generator=g).to(dev)
     w = _bf16(1 + 0.1 * torch.randn(H, generator=g)).to(dev)
     y = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
+    ssq = torch.full((rows,), float("nan"), device=dev)
     xr = x.clone()
     if S:
         acc = slabs[0].clone()
@@ -223,15 +230,146 @@ def test_residual_rmsnorm(lib, dev, S):
         xr = xr + acc
     x0 = x.clone()
     L.check(lib.ms_op_residual_rmsnorm(x.data_ptr(), slabs.data_ptr(), S, w.data_ptr(), y.data_ptr(),
-                                       rows, H, 1e-5, _stream()))
+                                       ssq.data_ptr(), rows, H, _stream()))
     torch.cuda.synchronize()
     assert torch.equal(x, xr) if S else torch.equal(x, x0)  # same adds in the same order
-    ref = xr * torch.rsqrt((xr * xr).mean(-1, keepdim=True) + 1e-5) * w.float()
-    assert rel(y.float().cpu(), ref.cpu()) < 5e-3
+    assert torch.equal(y, (xr * w.float()).to(torch.bfloat16))  # one RNE rounding of x * w
+    assert rel(ssq.double().cpu(), _ssq_ref(xr.cpu())) < 1e-6
     y2 = torch.empty_like(y)
-    L.check(lib.ms_op_rmsnorm(xr.data_ptr(), w.data_ptr(), y2.data_ptr(), rows, H, 1e-5, None, _stream()))
+    ssq2 = torch.empty_like(ssq)
+    L.check(lib.ms_op_rmsnorm(xr.data_ptr(), w.data_ptr(), y2.data_ptr(), ssq2.data_ptr(), rows, H, None,
+                              _stream()))
     torch.cuda.synchronize()
-    assert torch.equal(y, y2), "fused residual+norm must equal the plain norm of the same x"
+    assert torch.equal(y, y2), "fused residual+norm must give the plain norm's GEMM input"
+    assert rel(ssq2.double().cpu(), ssq.double().cpu()) < 1e-6  # its own fp32 sum order
+
+
+@pytest.mark.parametrize("M,rt", [(1, 12), (8, 12), (13, 16)])
+def test_gemv_resid_epilogue(lib, dev, M, rt):
+    """Decode O / down with the residual update fused (the engine's small-regime layer): x +=
+    X . W^T, xg = bf16(x * gamma), per-tile sums of the new x^2; a projection scaled from those
+    256 partial sums equals rmsnorm(x) * gamma . W^T (the deferred RMSNorm)."""
+    g = torch.Generator(device="cpu").manual_seed(M * 100 + rt)
+    N, K, eps = 3072, 3072, 1e-5
+    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
+    W = _bf16(torch.randn(N, K, generator=g) * 0.03).to(dev)
+    x = (torch.randn(M, N, generator=g) * 2).to(dev)
+    gamma = _bf16(1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    x_ref = x.double().cpu() + X.double().cpu() @ W.double().cpu().T
+    xg = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    tiles = N // rt
+    ssq = torch.full((tiles, M), float("nan"), device=dev)
+    L.check(lib.ms_op_gemv_resid(X.data_ptr(), W.data_ptr(), x.data_ptr(), xg.data_ptr(), gamma.data_ptr(),
+                                 ssq.data_ptr(), M, N, K, rt, _stream()))
+    torch.cuda.synchronize()
+    assert rel(x.double().cpu(), x_ref) < 1e-6
+    assert torch.equal(xg, (x * gamma.float()).to(torch.bfloat16))  # from the stored x exactly
+    for t in (0, tiles // 2, tiles - 1):
+        exp = (x[:, t * rt:(t + 1) * rt].double() ** 2).sum(-1).cpu()
+        assert rel(ssq[t].double().cpu(), exp) < 1e-6, t
+    # the consumer: QKV-like projection scaled by the 256-tile statistics
+    Wq = _bf16(torch.randn(1024, N, generator=g) * 0.03).to(dev)
+    out = torch.empty(M, 1024, device=dev)
+    ws = torch.zeros(256, dtype=torch.uint8, device=dev)
+    L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), tiles, N, eps))
+    try:
+        L.check(lib.ms_op_gemv(xg.data_ptr(), Wq.data_ptr(), out.data_ptr(), M, 1024, N, 1024, L.MS_EPI_STORE_F32,
+                               ws.data_ptr(), _stream()))
+    finally:
+        L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
+    torch.cuda.synchronize()
+    xd = x.double().cpu()
+    r = 1.0 / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
+    exp = r * (xg.double().cpu() @ Wq.double().cpu().T)
+    assert rel(out.double().cpu(), exp) < 1e-5
+
+
+@pytest.mark.parametrize("path", ["gemv", "gemv_split", "dgemm", "gemm", "qgemv"])
+def test_row_scale_epilogues(lib, dev, path):
+    """Every normalised-projection epilogue applies the deferred RMSNorm factor of its rows:
+    out[r] = rinv(r) * (X . W^T)[r], rinv = 1/sqrt(ssq[r] / H + eps) -- STORE_F32 slabs, SwiGLU
+    (gate and up both scaled before silu) and the argmax epilogue."""
+    g = torch.Generator(device="cpu").manual_seed(hash(path) % 1000)
+    M, K, eps = 8, 3072, 1e-5
+    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
+    ssq = (torch.rand(M, generator=g) * 5000 + 100).to(dev)
+    r = (1.0 / torch.sqrt(ssq.double().cpu() / K + eps))[:, None]
+    ws = torch.zeros(256, dtype=torch.uint8, device=dev)
+    L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), 1, K, eps))
+    try:
+        if path == "qgemv":
+            q4 = Q.GGML_TYPE_Q4_K
+            N = 512
+            blocks = Q.random_blocks(q4, N * K // 256, seed=3)
+            bf = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+            packed = torch.empty(N * (K // 256) * 144, dtype=torch.uint8, device=dev)
+            bl = torch.from_numpy(blocks.reshape(-1)).to(dev)
+            L.check(lib.ms_op_quant_rows(q4, bl.data_ptr(), N, K, bf.data_ptr(), packed.data_ptr(), _stream()))
+            out = torch.empty(M, N, device=dev)
+            L.check(lib.ms_op_qgemv(X.data_ptr(), q4, packed.data_ptr(), out.data_ptr(), M, N, K, N,
+                                    L.MS_EPI_STORE_F32, _stream()))
+            torch.cuda.synchronize()
+            deq = torch.empty(N * K, dtype=torch.float32, device=dev)
+            L.check(lib.ms_op_dequant(q4, bl.data_ptr(), N * K // 256, deq.data_ptr(), _stream()))
+            torch.cuda.synchronize()
+            exp = r * (X.double().cpu() @ deq.view(N, K).double().cpu().T)
+            assert rel(out.double().cpu(), exp) < 1e-5
+            return
+        N = 1024
+        W = _bf16(torch.randn(N, K, generator=g) * 0.03).to(dev)
+        exp = r * (X.double().cpu() @ W.double().cpu().T)
+        if path == "gemv_split":
+            S = 4
+            slabs = torch.empty(S, M, N, device=dev)
+            L.check(lib.ms_op_gemv_split(X.data_ptr(), W.data_ptr(), slabs.data_ptr(), M, N, K, S, 0, _stream()))
+            torch.cuda.synchronize()
+            assert rel(slabs.double().sum(0).cpu(), exp) < 1e-5
+            return
+        out = torch.empty(M, N, device=dev)
+        if path == "gemv":
+            L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, N, L.MS_EPI_STORE_F32,
+                                   ws.data_ptr(), _stream()))
+        elif path == "dgemm":
+            L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, 1, N, L.MS_EPI_STORE_F32,
+                                    _stream()))
+        else:
+            L.check(lib.ms_op_gemm(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, N, L.MS_EPI_STORE_F32,
+                                   _stream()))
+        torch.cuda.synchronize()
+        assert rel(out.double().cpu(), exp) < 1e-5
+        # SwiGLU (rows interleaved gate/up per 16): silu(r g) * (r u)
+        h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+        if path == "gemv":
+            L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), h.data_ptr(), M, N, K, N // 2, L.MS_EPI_SWIGLU,
+                                   ws.data_ptr(), _stream()))
+        elif path == "dgemm":
+            L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), h.data_ptr(), M, N, K, 1, N // 2, L.MS_EPI_SWIGLU,
+                                    _stream()))
+        else:
+            L.check(lib.ms_op_gemm(X.data_ptr(), W.data_ptr(), h.data_ptr(), M, N, K, N // 2, L.MS_EPI_SWIGLU,
+                                   _stream()))
+        torch.cuda.synchronize()
+        e4 = exp.view(M, N // 32, 2, 16)
+        gt, up = e4[:, :, 0, :].reshape(M, -1), e4[:, :, 1, :].reshape(M, -1)
+        sw = gt / (1 + torch.exp(-gt)) * up
+        assert rel(h.double().cpu(), sw) < 8e-3
+        if path in ("gemv", "dgemm"):  # argmax epilogue on scaled logits: r > 0 keeps the order
+            tiles = N // 16
+            part = torch.empty(M, tiles, 2, device=dev)
+            ids = torch.empty(M, dtype=torch.int32, device=dev)
+            if path == "gemv":
+                L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), part.data_ptr(), M, N, K, tiles,
+                                       L.MS_EPI_ARGMAX, ws.data_ptr(), _stream()))
+            else:
+                L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), part.data_ptr(), M, N, K, 1, tiles,
+                                        L.MS_EPI_ARGMAX, _stream()))
+            L.check(lib.ms_op_argmax_partials(part.data_ptr(), M, tiles, ids.data_ptr(), _stream()))
+            torch.cuda.synchronize()
+            assert ids.cpu().tolist() == torch.argmax(out.cpu(), 1).tolist()
+            mx = part[:, :, 0].max(1).values.double().cpu()
+            assert rel(mx, exp.max(1).values) < 1e-5
+    finally:
+        L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
 
 
 @pytest.mark.parametrize("M", [1, 8, 33])
@@ -278,10 +416,14 @@ def test_rmsnorm_and_argmax(lib, dev):
     x = (torch.randn(37, 768, generator=g) * 3).to(dev)
     w = _bf16(1 + 0.1 * torch.randn(768, generator=g)).to(dev)
     y = torch.empty(37, 768, dtype=torch.bfloat16, device=dev)
-    L.check(lib.ms_op_rmsnorm(x.data_ptr(), w.data_ptr(), y.data_ptr(), 37, 768, 1e-5, None, _stream()))
-    ref = x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-5) * w.float()
+    ssq = torch.empty(37, device=dev)
+    idx = torch.arange(36, -1, -1, dtype=torch.int32, device=dev)  # gathered rows, reversed
+    L.check(lib.ms_op_rmsnorm(x.data_ptr(), w.data_ptr(), y.data_ptr(), ssq.data_ptr(), 37, 768, idx.data_ptr(),
+                              _stream()))
     torch.cuda.synchronize()
-    assert rel(y.float().cpu(), ref.cpu()) < 5e-3
+    xs = x.flip(0)
+    assert torch.equal(y, (xs * w.float()).to(torch.bfloat16))
+    assert rel(ssq.double().cpu(), _ssq_ref(xs.cpu())) < 1e-6
     lg = torch.randn(5, 128256, generator=g).to(dev)
     lg[2, 77] = 100.0
     lg[2, 99] = 100.0  # tie -> lowest id
@@ -486,13 +628,13 @@ def test_errors_are_reported(dev):
         e.close()
 
 
-@pytest.mark.parametrize("slabs,fused", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
-    """The decode-attention variants (q/k/v from QKV split slabs or from the GEMV RoPE
-    epilogue; split combine in-launch -- write-through partials + arrival counter -- or as a
-    second launch) all agree with the oracle."""
+@pytest.mark.parametrize("slabs,resid", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_decode_attention_variants(oracle, monkeypatch, slabs, resid):
+    """The decode variants -- q/k/v from QKV split slabs or from the GEMV RoPE epilogue; O /
+    down adding into the residual in their epilogue (deferred-norm statistics from 256 column
+    tiles) or as split-K slabs + a residual_rmsnorm launch -- all agree with the oracle."""
     monkeypatch.setenv("MS_ATTN_SLABS", str(slabs))
-    monkeypatch.setenv("MS_ATTN_FUSED_COMBINE", str(fused))
+    monkeypatch.setenv("MS_RESID_FUSED", str(resid))
     e = Engine(TINY, device=0, max_batch=6, max_ctx=1024, max_prefill_tokens=4096)
     try:
         e.init_synthetic(SEED, STD, JITTER)
@@ -506,7 +648,7 @@ def test_decode_attention_variants(oracle, monkeypatch, slabs, fused):
             for pos, gap, top in flips:
                 assert gap <= 1e-2 * (abs(top) + 1.0), (pos, gap, top)
         assert agree / total >= 0.97, (agree, total)
-        # repeated launches reuse the zero-reset split tickets: same tokens again
+        # deterministic: the same tokens again
         again = e.generate(prompts, num_predict=16, ignore_eos=True)
         assert [r.ids for r in again] == [r.ids for r in res]
     finally:

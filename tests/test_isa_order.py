@@ -8,6 +8,8 @@ DMA would let the barrier pass with the X image still in flight.  This test disa
 the gfx950 code objects inside libmapsum.so and checks, for every LDS-staged GEMV
 instance, that no DMA follows a weight load before the barrier, and that the explicit wait
 in front of that barrier leaves no more loads outstanding than were issued after the DMA.
+(The deferred-norm partial sums, gemv_common.h rs_load, are 4-byte loads issued ahead of the
+DMA on purpose: older than both, they have landed whenever the DMA has.)
 """
 import os
 import re
@@ -77,7 +79,10 @@ def test_gemv_x_dma_precedes_weight_stream(tmp_path):
             dma = [k for k in range(first) if ops[k].startswith("global_load_lds")]
             wl = [k for k in range(first) if ops[k].startswith("global_load") and not ops[k].startswith("global_load_lds")]
             assert dma and wl, name
-            assert max(dma) < min(wl), f"{name}: a weight load was scheduled above the X DMA"
+            # loads above the last DMA may only be the <= 8 one-dword deferred-norm preloads
+            pre = [ops[k] for k in wl if k < max(dma)]
+            assert len(pre) <= 8 and all(o == "global_load_dword" for o in pre), \
+                f"{name}: a weight load was scheduled above the X DMA ({pre})"
             # the explicit wait in front of the barrier: vmcnt(N) with N <= loads issued after the DMA
             w = [k for k in range(max(dma), first) if ops[k] == "s_waitcnt" and "vmcnt" in ins[k]]
             assert w, f"{name}: no vmcnt wait between the X DMA and the barrier"
