@@ -270,7 +270,7 @@ struct ms_engine {
   }
 
   // the deferred RMSNorm scale of rows whose sums of squares a norm kernel wrote (one tile)
-  RowScale norm_rs() const { return RowScale{ssq, 1, H, cfg.norm_eps}; }
+  RowScale norm_rs() const { return make_row_scale(ssq, 1, H, cfg.norm_eps); }
 
   // normalised (rs) or plain projection: the decode GEMV where it fits, else the MFMA GEMM
   void gemm_or_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
@@ -372,7 +372,7 @@ struct ms_engine {
       launch_gemv_ex(X, W, x, B, H, K, H, MS_GEMV_EPI_RESID_SSQ, &ga, 0, stream);
       prof_end(K_GEMV);
       pending_split = 0;
-      cur_rs = RowScale{ssq, H / resid_rt, H, cfg.norm_eps};
+      cur_rs = make_row_scale(ssq, H / resid_rt, H, cfg.norm_eps);
     } else {
       pending_split = proj_split(q, X, W, B, H, K, S, Sl, nullptr);
       residual_norm(g_next, B);
@@ -687,6 +687,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
+    // the consumers stage the 256-tile statistics in LDS: engines of <= 16 slots (per engine,
+    // so every step of it runs the same arithmetic)
+    if (!gemv_rs_supported(cfg->max_batch, E.H / E.resid_rt)) E.resid_fuse = false;
     if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
     for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {
       c->args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
@@ -1193,7 +1196,7 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   // order is then the decode steps' one whatever the number of admitted prompts
   for (int r0 = 0; r0 < S; r0 += ms_engine::kMaxGemvRows) {
     const int rows = std::min(S - r0, (int)ms_engine::kMaxGemvRows);
-    const RowScale rs{E.ssq + r0, 1, E.H, E.cfg.norm_eps};
+    const RowScale rs = make_row_scale(E.ssq + r0, 1, E.H, E.cfg.norm_eps);
     E.gemm_or_gemv(E.xb + (size_t)r0 * E.H, E.lm_head, E.logits + (size_t)r0 * E.V, rows, E.V, E.H, E.V,
                    MS_EPI_STORE_F32, true, K_LMHEAD, &rs);
   }
@@ -1212,10 +1215,10 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
   PrefillAttnArgs pa{};
   E.prof_begin(K_MISC);
-  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream);
+  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream, E.layers[0].attn_norm, E.xb, E.ssq);
   E.prof_end(K_MISC);
   E.pending_split = 0;
-  E.residual_norm(E.layers[0].attn_norm, B);
+  E.cur_rs = E.norm_rs();
   // every layer leaves xb = bf16(x * the next gain) with its deferred scale in cur_rs
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   const RowScale rs = E.cur_rs;
@@ -1545,7 +1548,7 @@ static thread_local RowScale g_op_rs{};
 
 int ms_op_set_row_scale(const float* ssq, int32_t tiles, int32_t hidden, float eps) {
   if (ssq && (tiles < 1 || hidden < 1)) return MS_EINVAL;
-  g_op_rs = ssq ? RowScale{ssq, tiles, hidden, eps} : RowScale{};
+  g_op_rs = ssq ? make_row_scale(ssq, tiles, hidden, eps) : RowScale{};
   return MS_OK;
 }
 

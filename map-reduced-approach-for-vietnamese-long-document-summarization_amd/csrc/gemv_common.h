@@ -49,13 +49,13 @@ __device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict_
 // where a decode GEMV's MFMA takes its X fragments from (k_gemv.hip / k_qgemv.hip)
 enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
 
-// The deferred RMSNorm scale of a GEMV block's output rows (kernels.h RowScale).  The partial
-// sums [tiles][M] are copied into LDS by DMA at the very start of the kernel, ahead of the X copy
-// and the weight stream (no registers: a register preload cost the 1024-thread gate/up GEMV its
-// second co-resident block), and folded after the stream into rinv[row], which the epilogue
+// The deferred RMSNorm scale of a GEMV block's output rows (kernels.h RowScale), compiled only
+// into the instantiations that take one (template RS; the rest carry none of this code).  The
+// partial sums [tiles][M] are copied into LDS by DMA at the very start of the kernel, ahead of
+// the X copy and the weight stream (no registers: a register preload cost the 1024-thread
+// gate/up GEMV its second co-resident block), and folded into rinv[row], which the epilogue
 // reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order, then the
-// wave's xor tree.  Blocks with more than kRsStage partial sums read them from global memory
-// in the epilogue instead -- the same summation order, one memory round trip later.
+// wave's xor tree.  At most kRsStage partial sums (host-checked).
 constexpr int kRsStage = 4096;  // floats of partial sums a block stages in LDS (16 KiB)
 __host__ __device__ inline int rs_stage_floats(const RowScale& rs, int M) {
   const int n = rs.tiles * M;
@@ -69,7 +69,6 @@ __host__ __device__ inline size_t gemv_lds_total(size_t main_bytes, const RowSca
 }
 __device__ __forceinline__ void rs_dma(char* smem, size_t rinv_off, const RowScale& rs, int M) {
   const int nf = rs_stage_floats(rs, M);
-  if (nf == 0) return;  // block-uniform
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, n = rs.tiles * M;
   float* stage = (float*)(smem + rinv_off) + 64;
   for (int p = threadIdx.x >> 6; p * 64 < nf; p += nw)
@@ -77,19 +76,15 @@ __device__ __forceinline__ void rs_dma(char* smem, size_t rinv_off, const RowSca
                                      (LDS_AS void*)(stage + p * 64), 4, 0, 0);
 }
 // every wave calls this after a barrier that follows the DMA's completion (vmcnt); rinv[row]
-// for row < M once the caller's next barrier has passed
+// for row < M once the caller's next barrier has passed.  Staged statistics only (callers
+// check rs_stage_floats: the engine's are <= 256 tiles x 16 rows)
 __device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, const RowScale& rs, int M) {
-  if (!rs.ssq) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float* rinv = (float*)(smem + rinv_off);
   const float* stage = rinv + 64;
-  const bool staged = rs_stage_floats(rs, M) > 0;
   for (int row = wave; row < M; row += nw) {
     float sum = 0.f;
-    for (int t = lane; t < ((rs.tiles + 63) & ~63); t += 64) {
-      const int i = t * M + row;
-      sum += t < rs.tiles ? (staged ? stage[i] : rs.ssq[i]) : 0.f;
-    }
+    for (int t = lane; t < ((rs.tiles + 63) & ~63); t += 64) sum += t < rs.tiles ? stage[t * M + row] : 0.f;
     sum = wave_sum(sum);
     if (lane == 0) rinv[row] = rs_rinv(sum, rs);
   }
@@ -122,20 +117,52 @@ __device__ __forceinline__ void amax_merge_dev(float& v, int& i, float v2, int i
 
 // Cross-wave reduction of the per-wave MFMA accumulators through LDS and the epilogue.
 // acc[m][n][j] = C[row m*16 + 4*(lane>>4) + j][col n0 + n*16 + (lane&15)].
-template <int MT, int NT, int EPI>
+// RESID_SSQ: the x and gamma element each epilogue thread updates, loaded at kernel start
+// (ahead of the weight stream) so the epilogue itself waits on no memory
+struct ResidPre {
+  float x, g;
+};
+template <int MT, int NT, int EPI, bool RS>
 __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rinv, int M, int N, int ldo,
-                                              void* __restrict__ out, int n0, const GemvArgs& ga);
+                                              void* __restrict__ out, int n0, const GemvArgs& ga,
+                                              const ResidPre& pre);
+// element e of a tile result [mt][nt][lane][j] -> (row, col) of the output
+__device__ __forceinline__ void gemv_elem(int e, int NT, int n0, int& row, int& col, int& c) {
+  const int mn = e >> 8, l = (e >> 2) & 63, j = e & 3;
+  row = (mn / NT) * 16 + 4 * (l >> 4) + j;
+  c = l & 15;
+  col = n0 + (mn % NT) * 16 + c;
+}
+template <int EPI>
+__device__ __forceinline__ ResidPre resid_prefetch(int M, int N, int ldo, const void* out, int n0,
+                                                   const GemvArgs& ga) {
+  ResidPre p{0.f, 0.f};
+  if constexpr (EPI == MS_GEMV_EPI_RESID_SSQ) {
+    const int rtv = ga.rt > 0 ? ga.rt : 16;
+    if ((int)threadIdx.x < 256) {  // MT = NT = 1: one element per thread
+      int row, col, c;
+      gemv_elem(threadIdx.x, 1, n0, row, col, c);
+      if (row < M && c < rtv && col < N) {
+        p.x = ((const float*)out)[(size_t)row * ldo + col];
+        if (ga.xg_out) p.g = bf2f(ga.gamma[col]);
+      }
+    }
+  }
+  return p;
+}
 
-template <int MT, int NT, int EPI>
+// RS: the block's output rows carry a deferred-norm scale (ga.rs, staged by rs_dma); RS_DONE: the
+// kernel already folded the factors (rs_finish right after its X barrier, under the weights)
+template <int MT, int NT, int EPI, bool RS = false, bool RS_DONE = false>
 __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, size_t rinv_off,
                                             int M, int N, int ldo, void* __restrict__ out, int n0,
-                                            const GemvArgs& ga) {
+                                            const GemvArgs& ga, const ResidPre& pre = ResidPre{0.f, 0.f}) {
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* rinv = (const float*)(smem + rinv_off);
-  if (ga.rs.ssq) wait_vmcnt0();  // the staged partial sums (rs_dma) have landed
+  if constexpr (RS && !RS_DONE) wait_vmcnt0();  // the staged partial sums (rs_dma) have landed
   __syncthreads();  // X image no longer needed: reuse LDS for the partials
-  rs_finish(smem, rinv_off, ga.rs, M);
+  if constexpr (RS && !RS_DONE) rs_finish(smem, rinv_off, ga.rs, M);
   float* red = (float*)smem;
 #pragma unroll
   for (int m = 0; m < MT; ++m)
@@ -143,18 +170,18 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
     for (int n = 0; n < NT; ++n)
       *(f32x4*)&red[wave * ELEMS + ((m * NT + n) * 64 + lane) * 4] = acc[m][n];
   __syncthreads();
-  gemv_epilogue<MT, NT, EPI>(red, rinv, M, N, ldo, out, n0, ga);
+  gemv_epilogue<MT, NT, EPI, RS>(red, rinv, M, N, ldo, out, n0, ga, pre);
 }
 
 // The epilogue of a decode GEMV tile from the per-wave partials in LDS (red[wave][elem]).
-template <int MT, int NT, int EPI>
+template <int MT, int NT, int EPI, bool RS>
 __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rinv, int M, int N, int ldo,
-                                              void* __restrict__ out, int n0, const GemvArgs& ga) {
+                                              void* __restrict__ out, int n0, const GemvArgs& ga,
+                                              const ResidPre& pre) {
   constexpr int ELEMS = MT * NT * 256;
   const int tid = threadIdx.x;
   const int nthreads = blockDim.x, nw = nthreads >> 6;
-  const bool scaled = ga.rs.ssq != nullptr;  // block-uniform
-  auto rsc = [&](int row) { return scaled ? rinv[row] : 1.0f; };
+  auto rsc = [&](int row) { return RS ? rinv[row] : 1.0f; };
   // element e = ((m*NT + n)*64 + l)*4 + j -> row m*16 + 4*(l>>4) + j, col n0 + n*16 + (l&15)
   auto sum_e = [&](int e) {
     float v = 0.f;
@@ -221,10 +248,10 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
       float q = 0.f;
       if (row < M && c < rtv && col < N) {
         float* px = (float*)out + (size_t)row * ldo + col;
-        const float xo = *px + sum_e(e);
+        const float xo = (ELEMS <= 256 ? pre.x : *px) + sum_e(e);  // pre: resid_prefetch
         *px = xo;
         q = xo * xo;
-        if (ga.xg_out) ga.xg_out[(size_t)row * ldo + col] = f2bf(xo * bf2f(ga.gamma[col]));
+        if (ga.xg_out) ga.xg_out[(size_t)row * ldo + col] = f2bf(xo * (ELEMS <= 256 ? pre.g : bf2f(ga.gamma[col])));
       }
 #pragma unroll
       for (int o = 4; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);

@@ -389,6 +389,17 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   auto page_id = [&](int pg) { return kv.slot_major ? slot * kv.max_pages + pg : bt[pg]; };
   int pid_next = 0;
   if constexpr (PPWT == 2) pid_next = pg0 + NWB < pend ? page_id(pg0 + NWB) : 0;
+  // the row's deferred-norm partial sums (every wave folds them itself: no extra barrier),
+  // lane l holding tiles l + 64 i in order -- gemv_common.h rs_finish's summation order; loaded
+  // before the pages, so the fold waits on no page (vmcnt retires in order)
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  if (FROM_SLABS && qa.rs.ssq) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int t = lane + 64 * i;
+      rv[i] = t < qa.rs.tiles ? qa.rs.ssq[(size_t)t * a.B + b] : 0.f;
+    }
+  }
   // issue the first page first, so its HBM latency overlaps the q/k/v prologue
   if (pg0 < pend) {
     const int pid0 = page_id(pg0);
@@ -405,16 +416,6 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
     const float rsn = qa.sin_tab[(size_t)pos * 64 + (tid & 63)];
     const int nvec = (G + (owns_new ? 2 : 0)) * kHeadDim;
     constexpr int PER = ((kMaxGroup + 2) * kHeadDim + 255) / 256;
-    // the row's deferred-norm partial sums (every wave folds them itself: no extra barrier),
-    // lane l holding tiles l + 64 i in order -- gemv_common.h rs_finish's summation order
-    float rv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (qa.rs.ssq) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int t = lane + 64 * i;
-        rv[i] = t < qa.rs.tiles ? qa.rs.ssq[(size_t)t * a.B + b] : 0.f;
-      }
-    }
     float sv[PER][kMaxSlabs];  // every slab load of this thread in flight at once
 #pragma unroll
     for (int i = 0; i < PER; ++i) {

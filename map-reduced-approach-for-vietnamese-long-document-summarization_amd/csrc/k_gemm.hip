@@ -36,8 +36,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
                                                      const bf16_t* __restrict__ W,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, RowScale rs) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GBM * GBK * 2];  // 64 KiB
-  __shared__ float rinv_s[GBM];  // the tile rows' sums of squares (deferred-norm statistics)
+  // 64 KiB of tiles + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
+  // object: with the DMA into a second array the compiler drained vmcnt before every LDS read
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GBM * GBK * 2 + GBM * 4];
+  float* rinv_s = (float*)(smem + 2 * 2 * GBM * GBK * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
@@ -206,8 +208,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
                                                         const bf16_t* __restrict__ W,
                                                         void* __restrict__ out, int M, int N, int K,
                                                         int ldo, RowScale rs) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * 65536];
-  __shared__ float rinv_s[TBM];  // the tile rows' sums of squares (deferred-norm statistics)
+  // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
+  // object: with the DMA into a second array the compiler drained vmcnt before every LDS read
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4];
+  float* rinv_s = (float*)(smem + 2 * 65536);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (N + TBN - 1) / TBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);

@@ -80,11 +80,10 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds, const R
 //   kXRegs:   each wave loads its OWN k-slice of X (the only part it multiplies) straight
 //             into registers ahead of its weight loads -- no LDS image, no block barrier,
 //             every wave starts its MFMAs as soon as its own bytes have landed.
-// rinv_off: LDS byte offset of the deferred-norm factors (gemv_rinv_offset).
-// Plans of <= 6 register stages (gate/up: U = 3, NT = 2 on 512 blocks) are held to 64 VGPRs so
-// two 1024-thread blocks share a CU (launch bounds: 8 waves per SIMD).
-template <int MT, int NT, int EPI, int U, int XM>
-__global__ __launch_bounds__(1024, (MT == 1 && U * NT <= 6) ? 8 : 1) void gemv_kernel(const bf16_t* __restrict__ X,
+// rinv_off: LDS byte offset of the deferred-norm factors (gemv_rinv_offset).  (Two
+// 1024-thread gate/up blocks share a CU at <= 64 VGPRs: 58 / 60 without / with the row scale.)
+template <int MT, int NT, int EPI, int U, int XM, bool RS>
+__global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
                                                     const bf16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
                                                     int ldk, int ldo, int rinv_off, GemvArgs ga) {
@@ -103,7 +102,8 @@ __global__ __launch_bounds__(1024, (MT == 1 && U * NT <= 6) ? 8 : 1) void gemv_k
 
   // 0. the output rows' deferred-norm partial sums, 1. X (LDS DMA of the block's rows or this
   // wave's slice into registers), then this wave's whole W stream: vmcnt retires in issue order
-  rs_dma(smem, rinv_off, ga.rs, M);
+  if constexpr (RS) rs_dma(smem, rinv_off, ga.rs, M);
+  const ResidPre pre = resid_prefetch<EPI>(M, N, ldo, out, n0, ga);
   if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
   uint4 xr[XM == kXRegs ? U : 1][XM == kXRegs ? MT : 1][2];
   if constexpr (XM == kXRegs) {
@@ -128,11 +128,14 @@ __global__ __launch_bounds__(1024, (MT == 1 && U * NT <= 6) ? 8 : 1) void gemv_k
       w[u][n][1] = ldw16(wp + u * 64 + 8);
     }
   }
-  // 2. the X image has landed once at most the W loads are pending
+  // 2. the X image (and the staged row statistics, issued before it) has landed once at most
+  // the W loads are pending; the row factors are folded now, under the weight stream
   if constexpr (XM == kXLds) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
     __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the W loads too
+    // (two-tile plans fold them at the end: their 6 weight stages fill the 64 VGPRs)
+    if constexpr (RS && NT == 1) rs_finish(smem, rinv_off, ga.rs, M);
   }
 
   f32x4 acc[MT][NT];
@@ -165,7 +168,32 @@ __global__ __launch_bounds__(1024, (MT == 1 && U * NT <= 6) ? 8 : 1) void gemv_k
       }
     }
   }
-  gemv_finish<MT, NT, EPI>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
+  gemv_finish<MT, NT, EPI, RS, XM == kXLds && NT == 1>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, pre);
+}
+
+// the deferred row scale exists only for the epilogues of normalised projections
+template <int EPI> constexpr bool gemv_rs_epi() {
+  return EPI == MS_GEMV_EPI_STORE_BF16 || EPI == MS_GEMV_EPI_SWIGLU || EPI == MS_GEMV_EPI_STORE_F32 ||
+         EPI == MS_GEMV_EPI_ROPE_KV;
+}
+
+template <int MT, int NT, int EPI, int U, bool RS>
+static void gemv_go_rs(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+                       const dim3& grid, const dim3& blk, size_t lds, int ro, int ldo, int xm,
+                       const GemvArgs& ga, hipStream_t s) {
+  if constexpr (MT * U <= kXRegsMaxFrags) {
+    if (xm == kXRegs) {
+      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXRegs, RS>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+                ldo, ro, ga);
+      return;
+    }
+  }
+  if (xm == kXLds)
+    MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXLds, RS>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+              ldo, ro, ga);
+  else
+    MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXGlobal, RS>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
+              ldo, ro, ga);
 }
 
 template <int MT, int NT, int EPI, int U>
@@ -176,20 +204,11 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
   const int ro = (int)gemv_rinv_offset(gemv_lds_main(p, M, K, xm == kXLds));
   if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
     return;  // rope epilogue works on M <= 16 (checked by gemv_supported)
+  } else if constexpr (gemv_rs_epi<EPI>()) {
+    if (ga.rs.ssq) gemv_go_rs<MT, NT, EPI, U, true>(X, W, out, M, N, K, ldk, grid, blk, lds, ro, ldo, xm, ga, s);
+    else gemv_go_rs<MT, NT, EPI, U, false>(X, W, out, M, N, K, ldk, grid, blk, lds, ro, ldo, xm, ga, s);
   } else {
-    if constexpr (MT * U <= kXRegsMaxFrags) {
-      if (xm == kXRegs) {
-        MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXRegs>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                  ldo, ro, ga);
-        return;
-      }
-    }
-    if (xm == kXLds)
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXLds>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                ldo, ro, ga);
-    else
-      MS_LAUNCH((gemv_kernel<MT, NT, EPI, U, kXGlobal>), grid, blk, lds, s, X, W, out, M, N, K, ldk,
-                ldo, ro, ga);
+    gemv_go_rs<MT, NT, EPI, U, false>(X, W, out, M, N, K, ldk, grid, blk, lds, ro, ldo, xm, ga, s);
   }
 }
 
@@ -250,7 +269,9 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   if (gemv_x_regs() && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
-  if (epi == MS_GEMV_EPI_ARGMAX) ga.rs = RowScale{};  // r > 0 keeps every row's order
+  if (epi == MS_GEMV_EPI_ARGMAX || epi == MS_GEMV_EPI_ADD_F32 || epi == MS_GEMV_EPI_RESID_SSQ)
+    ga.rs = RowScale{};  // argmax: r > 0 keeps every row's order; the others take unnormalised X
+  if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds, ga.rs);
   if (lds > kMaxLds) return;
   switch (p.MT) {
@@ -271,6 +292,8 @@ void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int
                          int ldo, int epi, hipStream_t s) {
   gemv_dispatch(X, W, out, M, N, K, ldk, 1, ldo, epi, nullptr, 0, s);
 }
+
+bool gemv_rs_supported(int M, int tiles) { return M >= 1 && tiles >= 1 && tiles * M <= kRsStage; }
 
 bool gemv_split_supported(int M, int N, int K, int S) {
   if (S < 1 || K % S) return false;

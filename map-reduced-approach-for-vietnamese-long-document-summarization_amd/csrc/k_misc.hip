@@ -11,13 +11,18 @@ namespace ms {
 thread_local ProfEvents* g_prof = nullptr;
 
 // ---------------------------------------------------------------- embedding
-// x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores
+// x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores.  With gamma (a decode step's first
+// layer): also xg[t] = bf16(x[t] * gamma) and ssq[t] = sum of x[t]^2 (a fixed order)
+// -- the first QKV projection's input and deferred-norm statistics, with no norm launch.
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
                                                     const bf16_t* __restrict__ emb, int H,
-                                                    float* __restrict__ x) {
+                                                    float* __restrict__ x, const bf16_t* __restrict__ gamma,
+                                                    bf16_t* __restrict__ xg, float* __restrict__ ssq) {
+  __shared__ float red[4];
   const int t = blockIdx.x;
   const bf16_t* row = emb + (size_t)ids[t] * H;
   float* xo = x + (size_t)t * H;
+  float ss = 0.f;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     uint4 v = *(const uint4*)(row + c * 8);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -28,7 +33,23 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
     b.z = __uint_as_float(w[3] << 16); b.w = __uint_as_float(w[3] & 0xFFFF0000u);
     *(float4*)(xo + c * 8) = a;
     *(float4*)(xo + c * 8 + 4) = b;
+    if (gamma) {  // block-uniform
+      const uint4 gv = *(const uint4*)(gamma + c * 8);
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+      uint4 o;
+      o.x = pack2bf(a.x * __uint_as_float(gw[0] << 16), a.y * __uint_as_float(gw[0] & 0xFFFF0000u));
+      o.y = pack2bf(a.z * __uint_as_float(gw[1] << 16), a.w * __uint_as_float(gw[1] & 0xFFFF0000u));
+      o.z = pack2bf(b.x * __uint_as_float(gw[2] << 16), b.y * __uint_as_float(gw[2] & 0xFFFF0000u));
+      o.w = pack2bf(b.z * __uint_as_float(gw[3] << 16), b.w * __uint_as_float(gw[3] & 0xFFFF0000u));
+      *(uint4*)(xg + (size_t)t * H + c * 8) = o;
+      ss += (a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w);
+    }
   }
+  if (!gamma) return;
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  if (threadIdx.x == 0) ssq[t] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
 // Chained decode steps (engine.cpp decode_run): the step's argmax ids become the next
@@ -59,9 +80,10 @@ void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring,
   MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
 }
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s) {
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
+                  const bf16_t* gamma, bf16_t* xg, float* ssq) {
   if (T <= 0) return;
-  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x);
+  MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x, gamma, xg, ssq);
 }
 
 // ---------------------------------------------------------------- RMSNorm

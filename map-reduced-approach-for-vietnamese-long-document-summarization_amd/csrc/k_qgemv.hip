@@ -189,7 +189,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  rs_dma(smem, rinv_off, ga.rs, M);  // the output rows' deferred-norm sums, ahead of every load
+  if (ga.rs.ssq) rs_dma(smem, rinv_off, ga.rs, M);  // the rows' deferred-norm sums, ahead of every load
   // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
   // of the full row, where K is the per-split length; X and out shift to that slab.
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
@@ -348,7 +348,10 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         }
       }
   }
-  gemv_finish<MT, NT, EPI>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
+  if (ga.rs.ssq)  // block-uniform
+    gemv_finish<MT, NT, EPI, true>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
+  else
+    gemv_finish<MT, NT, EPI, false>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
 }
 
 struct QPlan {
@@ -398,7 +401,8 @@ template <int MT, int NT, int EPI>
 static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
                      const QPlan& p, const GemvArgs& ga_in, hipStream_t s, int S = 1) {
   GemvArgs ga = ga_in;
-  if (EPI == MS_GEMV_EPI_ARGMAX) ga.rs = RowScale{};  // r > 0 keeps every row's order
+  if (EPI == MS_GEMV_EPI_ARGMAX || EPI == MS_GEMV_EPI_ADD_F32) ga.rs = RowScale{};  // r > 0 keeps the order
+  if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = qlds(p, M, K, ga.rs);
   const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);

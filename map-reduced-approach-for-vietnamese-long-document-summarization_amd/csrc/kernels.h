@@ -36,7 +36,7 @@ struct DecodeAttnArgs {
 
 // The deferred RMSNorm of the numerics contract (oracle/llama_ref.py): a
 // normalised projection (QKV, gate/up, lm_head) multiplies the bf16 GEMM input bf16(x * g) by
-// W and scales output row r by rinv(r) = 1/sqrt(sum_t ssq[t][r] / H + eps), where ssq holds
+// W and scales output row r by rinv(r) = rsq(sum_t ssq[t][r] / H + eps), where ssq holds
 // partial sums of x[r]^2 [tiles][rows] written by the producer of x (a norm kernel: one tile;
 // a RESID_SSQ GEMV epilogue: one per column tile).  Every consumer forms the sum in the same
 // order (tile t = lane + 64 i added in i order per lane, then the wave's xor tree; with one
@@ -46,12 +46,21 @@ struct RowScale {
   const float* ssq;
   int tiles, H;
   float eps;
+  float inv_h;  // 1 / H
 };
-__host__ __device__ __forceinline__ float rs_rinv(float sum, const RowScale& rs) {
-  return 1.0f / sqrtf(sum / (float)rs.H + rs.eps);
+inline RowScale make_row_scale(const float* ssq, int tiles, int H, float eps) {
+  return RowScale{ssq, tiles, H, eps, 1.0f / (float)H};
+}
+// rinv = rsq(sum / H + eps): one v_rsq_f32 (1 ulp) -- the same instruction sequence in every
+// consumer, so every kernel derives the identical factor from the identical sum
+__device__ __forceinline__ float rs_rinv(float sum, const RowScale& rs) {
+  return __builtin_amdgcn_rsqf(__fmaf_rn(sum, rs.inv_h, rs.eps));
 }
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s);
+// x = the embedding rows; with gamma also xg = bf16(x * gamma) and ssq = per-row sums of x^2
+// (the first normalised projection's input, one-tile RowScale)
+void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
+                  const bf16_t* gamma = nullptr, bf16_t* xg = nullptr, float* ssq = nullptr);
 // chained decode: next ids <- this step's argmax (clamped into [0, V)), positions and key
 // counts += 1 in the step-argument blob [ids | positions | slots | key counts | step], and the
 // raw ids appended to ring row `step` (B <= 256)
@@ -114,6 +123,9 @@ struct GemvArgs {
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)
 bool gemv_split_supported(int M, int N, int K, int S);
+// whether a decode GEMV / Q-GEMV can take a deferred-norm scale of `tiles` partial sums per row
+// (staged in LDS: tiles * M <= 4096)
+bool gemv_rs_supported(int M, int tiles);
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga = nullptr);
 // X [M][ldk] and W [N][ldk] rows of stride ldk >= K (tuning hook: padded weight layouts)

@@ -8,8 +8,8 @@ DMA would let the barrier pass with the X image still in flight.  This test disa
 the gfx950 code objects inside libmapsum.so and checks, for every LDS-staged GEMV
 instance, that no DMA follows a weight load before the barrier, and that the explicit wait
 in front of that barrier leaves no more loads outstanding than were issued after the DMA.
-(The deferred-norm partial sums, gemv_common.h rs_load, are 4-byte loads issued ahead of the
-DMA on purpose: older than both, they have landed whenever the DMA has.)
+(The residual epilogue's x / gamma prefetch, gemv_common.h resid_prefetch, is issued ahead of
+the DMA on purpose: older than both, it has landed whenever the DMA has.)
 """
 import os
 import re
@@ -79,9 +79,10 @@ def test_gemv_x_dma_precedes_weight_stream(tmp_path):
             dma = [k for k in range(first) if ops[k].startswith("global_load_lds")]
             wl = [k for k in range(first) if ops[k].startswith("global_load") and not ops[k].startswith("global_load_lds")]
             assert dma and wl, name
-            # loads above the last DMA may only be the <= 8 one-dword deferred-norm preloads
+            # loads above the last DMA may only be the residual epilogue's x / gamma prefetch
+            # (gemv_common.h resid_prefetch: one dword, one bf16)
             pre = [ops[k] for k in wl if k < max(dma)]
-            assert len(pre) <= 8 and all(o == "global_load_dword" for o in pre), \
+            assert len(pre) <= 2 and all(o in ("global_load_dword", "global_load_ushort") for o in pre), \
                 f"{name}: a weight load was scheduled above the X DMA ({pre})"
             # the explicit wait in front of the barrier: vmcnt(N) with N <= loads issued after the DMA
             w = [k for k in range(max(dma), first) if ops[k] == "s_waitcnt" and "vmcnt" in ins[k]]
