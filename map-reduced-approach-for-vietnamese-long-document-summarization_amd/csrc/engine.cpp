@@ -136,7 +136,9 @@ struct ms_engine {
   // and per-tile sums of x^2 (ssq [256][B]) -- so the decode layer has no residual_rmsnorm
   // launch: the deferred RMSNorm (kernels.h RowScale) scales the rows of the QKV / gate-up /
   // lm_head outputs instead.  Chosen per engine (MS_RESID_FUSED=0: split-K slabs + norm
-  // launches, the K-quant and large-regime form).
+  // launches, the K-quant and large-regime form: the K-quant GEMV with this epilogue on 12-row
+  // tiles measured no faster than split-K 4 + residual_rmsnorm, 1.962 vs 1.955 ms per Q4_K_M
+  // decode step, profiles/r03/v7_q4_resid_fused_rejected.txt).
   bool resid_fuse = true, has_quant = false, warned_quant_large = false;
   int resid_rt = 12;
   bool resid_fused(const QSlot* q) const {
