@@ -52,14 +52,16 @@ enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
 // The deferred RMSNorm scale of a GEMV block's output rows (kernels.h RowScale), compiled only
 // into the instantiations that take one (template RS; the rest carry none of this code).  The
 // partial sums [tiles][M] are copied into LDS by DMA at the very start of the kernel, ahead of
-// the X copy and the weight stream (no registers: a register preload cost the 1024-thread
-// gate/up GEMV its second co-resident block), and folded into rinv[row], which the epilogue
-// reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order, then the
-// wave's xor tree.  At most kRsStage partial sums (host-checked).
+// the X copy and the weight stream (no registers: a register preload of 256 tiles cost the
+// 1024-thread gate/up GEMV its second co-resident block), and folded into rinv[row], which the
+// epilogue reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order,
+// then the wave's xor tree.  At most kRsStage partial sums (host-checked).  One-tile
+// statistics skip the stage: lane l of wave 0 loads ssq[l] into one register.
 constexpr int kRsStage = 4096;  // floats of partial sums a block stages in LDS (16 KiB)
+// one-tile statistics (a norm kernel's) need no staging: wave 0 loads them into a register
 __host__ __device__ inline int rs_stage_floats(const RowScale& rs, int M) {
   const int n = rs.tiles * M;
-  return (rs.ssq && n <= kRsStage) ? (n + 63) / 64 * 64 : 0;
+  return (rs.ssq && rs.tiles > 1 && n <= kRsStage) ? (n + 63) / 64 * 64 : 0;
 }
 // LDS of a decode GEMV block: [main: the X image or the per-wave partials, whichever is larger]
 // [rinv: 64 floats][staged partial sums]
@@ -67,20 +69,29 @@ __host__ __device__ inline size_t gemv_rinv_offset(size_t main_bytes) { return (
 __host__ __device__ inline size_t gemv_lds_total(size_t main_bytes, const RowScale& rs, int M) {
   return gemv_rinv_offset(main_bytes) + 64 * 4 + (size_t)rs_stage_floats(rs, M) * 4;
 }
-__device__ __forceinline__ void rs_dma(char* smem, size_t rinv_off, const RowScale& rs, int M) {
-  const int nf = rs_stage_floats(rs, M);
-  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6, n = rs.tiles * M;
+// issued before every other load of the kernel: one-tile statistics -> lane l of wave 0 holds
+// ssq[l] (returned); more tiles -> LDS DMA into the stage (returns 0)
+__device__ __forceinline__ float rs_begin(char* smem, size_t rinv_off, const RowScale& rs, int M) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (rs.tiles == 1) return (wave == 0 && lane < M) ? rs.ssq[lane] : 0.f;
+  const int nf = rs_stage_floats(rs, M), n = rs.tiles * M;
   float* stage = (float*)(smem + rinv_off) + 64;
-  for (int p = threadIdx.x >> 6; p * 64 < nf; p += nw)
+  for (int p = wave; p * 64 < nf; p += nw)
     __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(p * 64 + lane, n - 1)),
                                      (LDS_AS void*)(stage + p * 64), 4, 0, 0);
+  return 0.f;
 }
 // every wave calls this after a barrier that follows the DMA's completion (vmcnt); rinv[row]
-// for row < M once the caller's next barrier has passed.  Staged statistics only (callers
-// check rs_stage_floats: the engine's are <= 256 tiles x 16 rows)
-__device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, const RowScale& rs, int M) {
+// for row < M once the caller's next barrier has passed.  (Callers check rs_stage_floats: the
+// engine's are <= 256 tiles x 16 rows.)
+__device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, const RowScale& rs, int M,
+                                          float direct) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float* rinv = (float*)(smem + rinv_off);
+  if (rs.tiles == 1) {  // one partial: the wave tree of {ssq, 0, ..} is ssq itself
+    if (wave == 0 && lane < M) rinv[lane] = rs_rinv(direct, rs);
+    return;
+  }
   const float* stage = rinv + 64;
   for (int row = wave; row < M; row += nw) {
     float sum = 0.f;
@@ -88,6 +99,12 @@ __device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, con
     sum = wave_sum(sum);
     if (lane == 0) rinv[row] = rs_rinv(sum, rs);
   }
+}
+
+// the deferred row scale exists only for the epilogues of normalised projections
+template <int EPI> constexpr bool gemv_rs_epi() {
+  return EPI == MS_GEMV_EPI_STORE_BF16 || EPI == MS_GEMV_EPI_SWIGLU || EPI == MS_GEMV_EPI_STORE_F32 ||
+         EPI == MS_GEMV_EPI_ROPE_KV;
 }
 
 constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave may hold (<= 32 VGPRs)
@@ -151,18 +168,20 @@ __device__ __forceinline__ ResidPre resid_prefetch(int M, int N, int ldo, const 
   return p;
 }
 
-// RS: the block's output rows carry a deferred-norm scale (ga.rs, staged by rs_dma); RS_DONE: the
+// RS: the block's output rows carry a deferred-norm scale (ga.rs, rs_begin); RS_DONE: the
 // kernel already folded the factors (rs_finish right after its X barrier, under the weights)
 template <int MT, int NT, int EPI, bool RS = false, bool RS_DONE = false>
 __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, size_t rinv_off,
                                             int M, int N, int ldo, void* __restrict__ out, int n0,
-                                            const GemvArgs& ga, const ResidPre& pre = ResidPre{0.f, 0.f}) {
+                                            const GemvArgs& ga, const ResidPre& pre = ResidPre{0.f, 0.f},
+                                            float rs_direct = 0.f) {
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* rinv = (const float*)(smem + rinv_off);
-  if constexpr (RS && !RS_DONE) wait_vmcnt0();  // the staged partial sums (rs_dma) have landed
+  if constexpr (RS && !RS_DONE)
+    if (ga.rs.tiles > 1) wait_vmcnt0();  // the staged partial sums (rs_begin's DMA) have landed
   __syncthreads();  // X image no longer needed: reuse LDS for the partials
-  if constexpr (RS && !RS_DONE) rs_finish(smem, rinv_off, ga.rs, M);
+  if constexpr (RS && !RS_DONE) rs_finish(smem, rinv_off, ga.rs, M, rs_direct);
   float* red = (float*)smem;
 #pragma unroll
   for (int m = 0; m < MT; ++m)

@@ -184,12 +184,13 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 // MFMA t of a super-block takes 8 of those weights per lane and the X elements of the
 // same k -- a k permutation applied to both operands, so every dot product is unchanged.
 // XM: the X source (gemv_common.h kXGlobal / kXLds / kXRegs, as in k_gemv.hip)
-template <int MT, int NT, int EPI, int SBW, int XM>
+template <int MT, int NT, int EPI, int SBW, int XM, bool RS>
 __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  if (ga.rs.ssq) rs_dma(smem, rinv_off, ga.rs, M);  // the rows' deferred-norm sums, ahead of every load
+  float rsd = 0.f;  // the rows' deferred-norm statistics, ahead of every load
+  if constexpr (RS) rsd = rs_begin(smem, rinv_off, ga.rs, M);
   // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
   // of the full row, where K is the per-split length; X and out shift to that slab.
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
@@ -348,10 +349,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         }
       }
   }
-  if (ga.rs.ssq)  // block-uniform
-    gemv_finish<MT, NT, EPI, true>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
-  else
-    gemv_finish<MT, NT, EPI, false>(acc, smem, rinv_off, M, N, ldo, out, n0, ga);
+  gemv_finish<MT, NT, EPI, RS>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, ResidPre{0.f, 0.f}, rsd);
 }
 
 struct QPlan {
@@ -365,8 +363,6 @@ static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
   p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
   const int nsb = K / 256;
   p.SBW = nsb > 16 ? 2 : 1;
-  static const int env_sbw = [] { const char* v = getenv("MS_QSBW"); return v ? atoi(v) : 0; }();
-  if (env_sbw >= 1 && env_sbw <= 4 && nsb % env_sbw == 0 && nsb / env_sbw <= 16) p.SBW = env_sbw;  // tuning hook
   p.waves = (nsb % p.SBW == 0) ? nsb / p.SBW : 0;
   if (p.waves > 16) p.waves = 0;
   return p;
@@ -402,7 +398,7 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
                      const QPlan& p, const GemvArgs& ga_in, hipStream_t s, int S = 1) {
   GemvArgs ga = ga_in;
   if (EPI == MS_GEMV_EPI_ARGMAX || EPI == MS_GEMV_EPI_ADD_F32) ga.rs = RowScale{};  // r > 0 keeps the order
-  if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
+  if (ga.rs.ssq && ga.rs.tiles > 1 && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = qlds(p, M, K, ga.rs);
   const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
@@ -410,13 +406,20 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
     return;
   } else {
     const bool xl = qx_in_lds(M, K);
-#define QL(SBW_, XM_) \
-    MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ro, ga)
-    if (p.SBW == 4 && xl) QL(4, kXLds);
-    else if (p.SBW == 4) QL(4, kXGlobal);
-    else if (p.SBW == 3 && xl) QL(3, kXLds);
-    else if (p.SBW == 3) QL(3, kXGlobal);
-    else if (p.SBW == 2 && xl) QL(2, kXLds);
+    constexpr bool kRsEpi = gemv_rs_epi<EPI>();
+    const bool rs = kRsEpi && ga.rs.ssq != nullptr;
+#define QL(SBW_, XM_)                                                                                         \
+    do {                                                                                                      \
+      if constexpr (kRsEpi) {                                                                                 \
+        if (rs) {                                                                                             \
+          MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_, true>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ro, \
+                    ga);                                                                                      \
+          break;                                                                                              \
+        }                                                                                                     \
+      }                                                                                                       \
+      MS_LAUNCH((qgemv_kernel<MT, NT, EPI, SBW_, XM_, false>), grid, blk, lds, s, X, q, out, M, N, K, ldo, ro, ga); \
+    } while (0)
+    if (p.SBW == 2 && xl) QL(2, kXLds);
     else if (p.SBW == 2) QL(2, kXGlobal);
     else if (xl && !qx_in_regs(p)) QL(1, kXLds);
     else if (!qx_in_regs(p)) QL(1, kXGlobal);

@@ -69,8 +69,8 @@ def test_gemv_x_dma_precedes_weight_stream(tmp_path):
     checked = 0
     for co in _code_objects(LIB):
         for name, ins in _functions(co, str(tmp_path)).items():
-            # LDS-staged instances only: gemv_kernel<..., XM=kXLds>, qgemv_kernel<..., XM=kXLds>
-            if not re.search(r"q?gemv_kernelI.*Li1EEEv", name):
+            # LDS-staged instances only: gemv_kernel<..., XM=kXLds, RS>, qgemv_kernel<..., XM=kXLds, RS>
+            if not re.search(r"q?gemv_kernelI.*Li1ELb[01]EEEv", name):
                 continue
             ops = [i.split()[0] for i in ins]
             bar = [k for k, o in enumerate(ops) if o == "s_barrier"]
