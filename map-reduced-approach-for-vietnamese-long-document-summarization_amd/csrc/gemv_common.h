@@ -55,13 +55,15 @@ enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
 // the X copy and the weight stream (no registers: a register preload of 256 tiles cost the
 // 1024-thread gate/up GEMV its second co-resident block), and folded into rinv[row], which the
 // epilogue reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order,
-// then the wave's xor tree.  At most kRsStage partial sums (host-checked).  One-tile
-// statistics skip the stage: lane l of wave 0 loads ssq[l] into one register.
+// then the wave's xor tree.  At most kRsStage partial sums (host-checked).  HOLD kernels (the
+// K-quant GEMV) take one-tile statistics straight into a register of wave 0 instead; the bf16
+// GEMV stages them like any other: holding that register across the weight
+// stream took the 1024-thread gate/up GEMV from 63 to 67 VGPRs and cost its second co-resident
+// block (20.8 -> 22.4 us per launch, profiles/r03/v9_rs_hold_ab.txt).
 constexpr int kRsStage = 4096;  // floats of partial sums a block stages in LDS (16 KiB)
-// one-tile statistics (a norm kernel's) need no staging: wave 0 loads them into a register
 __host__ __device__ inline int rs_stage_floats(const RowScale& rs, int M) {
   const int n = rs.tiles * M;
-  return (rs.ssq && rs.tiles > 1 && n <= kRsStage) ? (n + 63) / 64 * 64 : 0;
+  return (rs.ssq && n <= kRsStage) ? (n + 63) / 64 * 64 : 0;
 }
 // LDS of a decode GEMV block: [main: the X image or the per-wave partials, whichever is larger]
 // [rinv: 64 floats][staged partial sums]
@@ -69,11 +71,13 @@ __host__ __device__ inline size_t gemv_rinv_offset(size_t main_bytes) { return (
 __host__ __device__ inline size_t gemv_lds_total(size_t main_bytes, const RowScale& rs, int M) {
   return gemv_rinv_offset(main_bytes) + 64 * 4 + (size_t)rs_stage_floats(rs, M) * 4;
 }
-// issued before every other load of the kernel: one-tile statistics -> lane l of wave 0 holds
-// ssq[l] (returned); more tiles -> LDS DMA into the stage (returns 0)
+// issued before every other load of the kernel: HOLD and one-tile statistics -> lane l of wave 0
+// holds ssq[l] (returned); otherwise LDS DMA into the stage (returns 0)
+template <bool HOLD>
 __device__ __forceinline__ float rs_begin(char* smem, size_t rinv_off, const RowScale& rs, int M) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  if (rs.tiles == 1) return (wave == 0 && lane < M) ? rs.ssq[lane] : 0.f;
+  if constexpr (HOLD)
+    if (rs.tiles == 1) return (wave == 0 && lane < M) ? rs.ssq[lane] : 0.f;
   const int nf = rs_stage_floats(rs, M), n = rs.tiles * M;
   float* stage = (float*)(smem + rinv_off) + 64;
   for (int p = wave; p * 64 < nf; p += nw)
@@ -84,11 +88,12 @@ __device__ __forceinline__ float rs_begin(char* smem, size_t rinv_off, const Row
 // every wave calls this after a barrier that follows the DMA's completion (vmcnt); rinv[row]
 // for row < M once the caller's next barrier has passed.  (Callers check rs_stage_floats: the
 // engine's are <= 256 tiles x 16 rows.)
+template <bool HOLD>
 __device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, const RowScale& rs, int M,
                                           float direct) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   float* rinv = (float*)(smem + rinv_off);
-  if (rs.tiles == 1) {  // one partial: the wave tree of {ssq, 0, ..} is ssq itself
+  if (HOLD && rs.tiles == 1) {  // one partial: the wave tree of {ssq, 0, ..} is ssq itself
     if (wave == 0 && lane < M) rinv[lane] = rs_rinv(direct, rs);
     return;
   }
@@ -169,8 +174,9 @@ __device__ __forceinline__ ResidPre resid_prefetch(int M, int N, int ldo, const 
 }
 
 // RS: the block's output rows carry a deferred-norm scale (ga.rs, rs_begin); RS_DONE: the
-// kernel already folded the factors (rs_finish right after its X barrier, under the weights)
-template <int MT, int NT, int EPI, bool RS = false, bool RS_DONE = false>
+// kernel already folded the factors (rs_finish right after its X barrier, under the weights);
+// RS_HOLD: rs_begin held one-tile statistics in the register passed as rs_direct
+template <int MT, int NT, int EPI, bool RS = false, bool RS_DONE = false, bool RS_HOLD = true>
 __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* smem, size_t rinv_off,
                                             int M, int N, int ldo, void* __restrict__ out, int n0,
                                             const GemvArgs& ga, const ResidPre& pre = ResidPre{0.f, 0.f},
@@ -178,10 +184,9 @@ __device__ __forceinline__ void gemv_finish(const f32x4 (&acc)[MT][NT], char* sm
   constexpr int ELEMS = MT * NT * 256;  // floats per wave result [mt][nt][lane][j]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const float* rinv = (const float*)(smem + rinv_off);
-  if constexpr (RS && !RS_DONE)
-    if (ga.rs.tiles > 1) wait_vmcnt0();  // the staged partial sums (rs_begin's DMA) have landed
+  if constexpr (RS && !RS_DONE) wait_vmcnt0();  // the staged partial sums (rs_begin's DMA) have landed
   __syncthreads();  // X image no longer needed: reuse LDS for the partials
-  if constexpr (RS && !RS_DONE) rs_finish(smem, rinv_off, ga.rs, M, rs_direct);
+  if constexpr (RS && !RS_DONE) rs_finish<RS_HOLD>(smem, rinv_off, ga.rs, M, rs_direct);
   float* red = (float*)smem;
 #pragma unroll
   for (int m = 0; m < MT; ++m)

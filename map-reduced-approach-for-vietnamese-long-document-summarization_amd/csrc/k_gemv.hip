@@ -102,8 +102,9 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 
   // 0. the output rows' deferred-norm partial sums, 1. X (LDS DMA of the block's rows or this
   // wave's slice into registers), then this wave's whole W stream: vmcnt retires in issue order
-  float rsd = 0.f;
-  if constexpr (RS) rsd = rs_begin(smem, rinv_off, ga.rs, M);
+  // (row statistics always staged here: gemv_common.h rs_begin HOLD)
+  constexpr bool kRsEarly = XM == kXLds && NT == 1;  // folds right after the X barrier
+  if constexpr (RS) rs_begin<false>(smem, rinv_off, ga.rs, M);
   const ResidPre pre = resid_prefetch<EPI>(M, N, ldo, out, n0, ga);
   if constexpr (XM == kXLds) gemv_dma_x(smem, X, M, K, ldk);
   uint4 xr[XM == kXRegs ? U : 1][XM == kXRegs ? MT : 1][2];
@@ -136,7 +137,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     __builtin_amdgcn_s_waitcnt(vmcnt_imm(U * NT * 2));
     __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the W loads too
     // (two-tile plans fold them at the end: their 6 weight stages fill the 64 VGPRs)
-    if constexpr (RS && NT == 1) rs_finish(smem, rinv_off, ga.rs, M, rsd);
+    if constexpr (RS && NT == 1) rs_finish<false>(smem, rinv_off, ga.rs, M, 0.f);
   }
 
   f32x4 acc[MT][NT];
@@ -169,7 +170,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
       }
     }
   }
-  gemv_finish<MT, NT, EPI, RS, XM == kXLds && NT == 1>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, pre, rsd);
+  gemv_finish<MT, NT, EPI, RS, kRsEarly, false>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, pre);
 }
 
 template <int MT, int NT, int EPI, int U, bool RS>
@@ -266,7 +267,7 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   if (ga_in) ga = *ga_in;
   if (epi == MS_GEMV_EPI_ARGMAX || epi == MS_GEMV_EPI_ADD_F32 || epi == MS_GEMV_EPI_RESID_SSQ)
     ga.rs = RowScale{};  // argmax: r > 0 keeps every row's order; the others take unnormalised X
-  if (ga.rs.ssq && ga.rs.tiles > 1 && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
+  if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds, ga.rs);
   if (lds > kMaxLds) return;
   switch (p.MT) {

@@ -190,7 +190,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
                                                      int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float rsd = 0.f;  // the rows' deferred-norm statistics, ahead of every load
-  if constexpr (RS) rsd = rs_begin(smem, rinv_off, ga.rs, M);
+  if constexpr (RS) rsd = rs_begin<true>(smem, rinv_off, ga.rs, M);
   // split-K (fp32 slab epilogue only): block row y owns super-blocks [y*K/256, (y+1)*K/256)
   // of the full row, where K is the per-split length; X and out shift to that slab.
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
@@ -398,7 +398,7 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
                      const QPlan& p, const GemvArgs& ga_in, hipStream_t s, int S = 1) {
   GemvArgs ga = ga_in;
   if (EPI == MS_GEMV_EPI_ARGMAX || EPI == MS_GEMV_EPI_ADD_F32) ga.rs = RowScale{};  // r > 0 keeps the order
-  if (ga.rs.ssq && ga.rs.tiles > 1 && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
+  if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = qlds(p, M, K, ga.rs);
   const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
