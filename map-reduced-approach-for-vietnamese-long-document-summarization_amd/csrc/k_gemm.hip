@@ -146,13 +146,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
     }
     return;
   }
+  f32x4 rv4[4];  // the rows' norm factors, as gemm256_kernel's epilogue
+#pragma unroll
+  for (int m = 0; m < 4; ++m) rv4[m] = f32x4{1.f, 1.f, 1.f, 1.f};
+  if (rs.ssq) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) rv4[m] = *(const f32x4*)(rinv_s + wm * 64 + m * 16 + fg * 4);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rv4[m][j] = rs_rinv(rv4[m][j], rs);
+  }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
       if (row >= M) continue;
-      const float rv = rs.ssq ? rs_rinv(rinv_s[wm * 64 + m * 16 + fg * 4 + j], rs) : 1.0f;
+      const float rv = rv4[m][j];
       if constexpr (EPI == 2) {  // SwiGLU: n even = gate, n odd = up of the same 16 features
 #pragma unroll
         for (int n = 0; n < 4; n += 2) {
@@ -379,13 +390,27 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
     }
     return;
   }
+  // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
+  // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
+  // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
+  f32x4 rv4[8];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) rv4[mi] = f32x4{1.f, 1.f, 1.f, 1.f};
+  if (rs.ssq) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) rv4[mi] = *(const f32x4*)(rinv_s + wr * 128 + mi * 16 + fg * 4);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
+  }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
       if (row >= M) continue;
-      const float rv = rs.ssq ? rs_rinv(rinv_s[wr * 128 + mi * 16 + fg * 4 + j], rs) : 1.0f;
+      const float rv = rv4[mi][j];
       if constexpr (EPI == 2) {  // SwiGLU: ni even = gate, ni odd = up of the same 16 features
 #pragma unroll
         for (int ni = 0; ni < 4; ni += 2) {

@@ -217,9 +217,12 @@ def bench_camp(lib, M):
         print(line, flush=True)
 
 
-def bench_gemm(lib):
+def bench_gemm(lib, rs=False, variants=(1, 2)):
+    """rs: the normalised projections (epi 0 / 2) take a one-tile deferred-norm row scale, as
+    in prefill (ms_op_set_row_scale; needs a library that has it)"""
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
+    ssq = (torch.rand(16384, device=dev) * 3072 + 1.0).float()
     for name, M, N, K, epi in [("qkv", 16384, 5120, 3072, 0), ("o", 16384, 3072, 3072, 1),
                                ("gu", 16384, 16384, 3072, 2), ("down", 16384, 3072, 8192, 1),
                                ("sq4k", 4096, 4096, 4096, 0)]:
@@ -230,8 +233,10 @@ def bench_gemm(lib):
         ldo = N if epi != 2 else N // 2
 
         def fn():
+            if rs:
+                lib.ms_op_set_row_scale(ssq.data_ptr() if epi in (0, 2) else None, 1, K, 1e-5)
             lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st)
-        for variant in (1, 2):
+        for variant in variants:
             lib.ms_set_gemm_variant(variant)
             t = timeit(fn, reps=5, rounds=3)
             print(f"gemm v{variant} {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s",
@@ -243,6 +248,8 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp"])
     ap.add_argument("--m", type=int, default=8)
+    ap.add_argument("--rs", action="store_true", help="gemm: deferred-norm row scale on epi 0 / 2")
+    ap.add_argument("--variants", default="1,2", help="gemm: tile variants (1: 128x128, 2: 256x256)")
     a = ap.parse_args()
     lib = L.load()
     if a.what == "gemv":
@@ -258,4 +265,4 @@ if __name__ == "__main__":
     elif a.what == "camp":
         bench_camp(lib, a.m)
     else:
-        bench_gemm(lib)
+        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")))
