@@ -322,19 +322,24 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
           const int k4 = t >> 1, sub = t & 1;
           const int si = hh * 8 + p + 2 * k4;
           const float ds = __fmul_rn(d, (float)(int)(int8_t)byte_of(sc[j][n], si));
+          const float nds = -32.0f * ds;  // exact (a power-of-two multiple of an fp16 x int8 product)
+          // the 6-bit codes of 4 weights assembled as bytes of one word (nibble | 2 high bits
+          // << 4), each byte converted straight to fp32 (v_cvt_f32_ubyte*), then
+          // fma(ds, q, -32 ds) = ds * (q - 32) with the single rounding of ggml's product (only
+          // the sign of an exact zero can differ); ~3 VALU per weight instead of ~7
+          const uint4 qsrc = (k4 & 1) ? qb[j][n] : qa[j][n];
           uint32_t pk[4];
 #pragma unroll
-          for (int i = 0; i < 8; i += 2) {
-            float y[2];
+          for (int w = 0; w < 2; ++w) {
+            const int wi = 2 * sub + w;  // weights li = 4 wi .. 4 wi + 3
+            const uint32_t aw = wi == 0 ? qsrc.x : wi == 1 ? qsrc.y : wi == 2 ? qsrc.z : qsrc.w;
+            const uint32_t hw = wi == 0 ? qh[j][n].x : wi == 1 ? qh[j][n].y : wi == 2 ? qh[j][n].z : qh[j][n].w;
+            const uint32_t q4 = (((k4 >> 1) ? (aw >> 4) : aw) & 0x0F0F0F0Fu) | (((hw >> (2 * k4)) & 0x03030303u) << 4);
+            float y[4];
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int li = 8 * sub + i + e;
-              const uint32_t a = byte_of((k4 & 1) ? qb[j][n] : qa[j][n], li);
-              const uint32_t hb = byte_of(qh[j][n], li);
-              const int q = (int)(((k4 >> 1) ? (a >> 4) : (a & 0xF)) | (((hb >> (2 * k4)) & 3) << 4)) - 32;
-              y[e] = __fmul_rn(ds, (float)q);
-            }
-            pk[i >> 1] = pack2bf(y[0], y[1]);
+            for (int b = 0; b < 4; ++b) y[b] = __fmaf_rn(ds, (float)((q4 >> (8 * b)) & 0xFFu), nds);
+            pk[2 * w] = pack2bf(y[0], y[1]);
+            pk[2 * w + 1] = pack2bf(y[2], y[3]);
           }
           const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
           const int k = (sb0 + j) * 256 + hh * 128 + k4 * 32 + 16 * p + 8 * sub;
