@@ -335,11 +335,12 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
             const uint32_t aw = wi == 0 ? qsrc.x : wi == 1 ? qsrc.y : wi == 2 ? qsrc.z : qsrc.w;
             const uint32_t hw = wi == 0 ? qh[j][n].x : wi == 1 ? qh[j][n].y : wi == 2 ? qh[j][n].z : qh[j][n].w;
             const uint32_t q4 = (((k4 >> 1) ? (aw >> 4) : aw) & 0x0F0F0F0Fu) | (((hw >> (2 * k4)) & 0x03030303u) << 4);
-            float y[4];
-#pragma unroll
-            for (int b = 0; b < 4; ++b) y[b] = __fmaf_rn(ds, (float)((q4 >> (8 * b)) & 0xFFu), nds);
-            pk[2 * w] = pack2bf(y[0], y[1]);
-            pk[2 * w + 1] = pack2bf(y[2], y[3]);
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const f2 ds2 = {ds, ds}, nds2 = {nds, nds};  // two weights per v_pk_fma_f32
+            const f2 y01 = __builtin_elementwise_fma(ds2, f2{(float)(q4 & 0xFFu), (float)((q4 >> 8) & 0xFFu)}, nds2);
+            const f2 y23 = __builtin_elementwise_fma(ds2, f2{(float)((q4 >> 16) & 0xFFu), (float)(q4 >> 24)}, nds2);
+            pk[2 * w] = pack2bf(y01.x, y01.y);
+            pk[2 * w + 1] = pack2bf(y23.x, y23.y);
           }
           const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
           const int k = (sb0 + j) * 256 + hh * 128 + k4 * 32 + 16 * p + 8 * sub;
