@@ -274,14 +274,13 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 }
 
 // ============================================================ decode (split-K over keys)
-// grid (B, Hk, nsplit); block 256 = 4 waves, ONE 64-key page per wave, so a block covers
-// 256 keys and every wave has its whole page (K as MFMA fragments + V rows, 32 KB)
-// in flight before its first MFMA.  The G query heads of the kv head are MFMA columns
-// 0..G-1.  Per-wave (m, l, O^T) are merged in LDS (reusing the waves' V images); each block
-// writes one partial (m, l, o[128]) per (b, q head, split), and the LAST block of a
-// (b, kv head) to finish (arrival counter with write-through partials,
-// cdna_hip_programming.md §6 Guideline 16) combines the nsplit partials and writes the bf16
-// output -- no second launch.
+// grid (B, Hk, nsplit); block 256 = 4 waves, each wave walking ppw 64-key pages (below) with
+// a whole page (K as MFMA fragments + V rows, 32 KB) in flight before its first MFMA.  The G
+// query heads of the kv head are MFMA columns 0..G-1.  Per-wave (m, l, O^T) are merged in LDS
+// (reusing the waves' V images); each block writes one partial (m, l, o[128]) per (b, q head,
+// split), and attn_decode_combine_kernel merges the nsplit partials into the bf16 output.
+// With the deferred RMSNorm (kernels.h RowScale) the prologue also folds the row's norm
+// statistics and scales q / k / v by r before rounding them.
 //
 // FROM_SLABS (the fused decode chain): the QKV projection arrives as S fp32 split-K slabs
 // [S][B][(Hq+2Hk)*128] with Q/K rows rope-permuted (k_gemv.hip).  The prologue adds the
