@@ -117,7 +117,7 @@ constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave 
 // the K-quant GEMVs take X into registers (Q4_K_M decode 2.023 -> 1.950 ms/step: the dequant
 // work of each wave starts as soon as its own bytes land, with no block barrier), the bf16
 // GEMVs keep the LDS image (registers measured 2.25 -> 2.39 ms/step).  MS_GEMV_X=regs /
-// MS_QGEMV_X=lds flip them (A/B tuning).
+// MS_QGEMV_X (below) flip them (A/B tuning).
 inline bool gemv_x_regs() {
   static const bool v = [] {
     const char* e = getenv("MS_GEMV_X");
@@ -125,10 +125,17 @@ inline bool gemv_x_regs() {
   }();
   return v;
 }
-inline bool qgemv_x_regs() {
-  static const bool v = [] {
+// K-quant X source (MS_QGEMV_X): 0 registers everywhere ("regs"), 1 LDS everywhere ("lds"),
+// 2 registers for the gate/up GEMV only ("gu", the default), 3 registers for all but gate/up
+// ("slab").  Same box, Q4_K_M decode ms/step: regs 1.862, lds 1.892, gu 1.845, slab 1.909
+// (profiles/r03/v15_qgemv_x_mode_ab.txt): the two-tile gate/up blocks start their dequant as
+// their own X lands; the one-tile slab / lm_head blocks (80 / 70 VGPRs with X in registers)
+// do better with the LDS image.
+inline int qgemv_x_mode() {
+  static const int v = [] {
     const char* e = getenv("MS_QGEMV_X");
-    return !(e && e[0] == 'l');
+    if (!e) return 2;
+    return e[0] == 'r' ? 0 : e[0] == 'l' ? 1 : e[0] == 'g' ? 2 : e[0] == 's' ? 3 : 2;
   }();
   return v;
 }

@@ -380,7 +380,11 @@ static bool qx_in_lds(int M, int K) {
   return gemv_x_lds_bytes(M, K) <= kLdsCap;
 }
 
-static bool qx_in_regs(const QPlan& p) { return qgemv_x_regs() && p.MT * p.SBW == 1; }
+static bool qx_in_regs(const QPlan& p) {
+  const int m = qgemv_x_mode();
+  const bool want = m == 0 || (m == 2 && p.NT == 2) || (m == 3 && p.NT != 2);
+  return want && p.MT * p.SBW == 1;
+}
 
 static size_t qlds_main(const QPlan& p, int M, int K) {
   // X image (when it fits and X is not taken into registers)
