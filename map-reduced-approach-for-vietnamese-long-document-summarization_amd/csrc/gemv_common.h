@@ -118,12 +118,24 @@ constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave 
 // work of each wave starts as soon as its own bytes land, with no block barrier), the bf16
 // GEMVs keep the LDS image (registers measured 2.25 -> 2.39 ms/step).  MS_GEMV_X=regs /
 // MS_QGEMV_X (below) flip them (A/B tuning).
-inline bool gemv_x_regs() {
-  static const bool v = [] {
+// bf16 X source (MS_GEMV_X): "lds" everywhere (default), "regs" everywhere (where MT x U fits),
+// "f32" registers for the split-K slab GEMVs only, "resid" for the residual-epilogue GEMVs only,
+// "both" for those two families
+enum { kGxLds = 0, kGxRegs = 1, kGxF32 = 2, kGxResid = 3, kGxBoth = 4 };
+inline int gemv_x_mode() {
+  static const int v = [] {
     const char* e = getenv("MS_GEMV_X");
-    return e && e[0] == 'r';
+    if (!e) return kGxLds;
+    const char c = e[0];
+    return c == 'r' && e[1] == 'e' && e[2] == 'g' ? kGxRegs : c == 'f' ? kGxF32 : c == 'r' ? kGxResid
+         : c == 'b' ? kGxBoth : kGxLds;
   }();
   return v;
+}
+inline bool gemv_x_regs_for(int epi) {
+  const int m = gemv_x_mode();
+  const bool f32 = epi == MS_GEMV_EPI_STORE_F32, resid = epi == MS_GEMV_EPI_RESID_SSQ;
+  return m == kGxRegs || ((m == kGxF32 || m == kGxBoth) && f32) || ((m == kGxResid || m == kGxBoth) && resid);
 }
 // K-quant X source (MS_QGEMV_X): 0 registers everywhere ("regs"), 1 LDS everywhere ("lds"),
 // 2 registers for the gate/up GEMV only ("gu", the default), 3 registers for all but gate/up

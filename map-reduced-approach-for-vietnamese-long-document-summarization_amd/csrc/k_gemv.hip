@@ -262,7 +262,7 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   if (p.waves == 0) return;  // callers check gemv_supported()
   const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
   int xm = xl ? kXLds : kXGlobal;
-  if (gemv_x_regs() && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
+  if (gemv_x_regs_for(epi) && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
   if (epi == MS_GEMV_EPI_ARGMAX || epi == MS_GEMV_EPI_ADD_F32 || epi == MS_GEMV_EPI_RESID_SSQ)
