@@ -1554,6 +1554,8 @@ int ms_op_set_row_scale(const float* ssq, int32_t tiles, int32_t hidden, float e
   return MS_OK;
 }
 
+static int op_rs_tiles() { return g_op_rs.ssq ? g_op_rs.tiles : 0; }
+
 static const GemvArgs* op_gemv_args(GemvArgs& ga) {
   ga = GemvArgs{};
   ga.rs = g_op_rs;
@@ -1592,7 +1594,9 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
     REQUIRE(X && W && out && ws && N >= 16 && N % 16 == 0, MS_EINVAL, "bad gemv operands");
     REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0),
             MS_EINVAL, "bad epilogue");
-    REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps)");
+    REQUIRE(gemv_supported(M, N, K, epi, op_rs_tiles()), MS_EINVAL,
+            "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps; "
+            "row-scale statistics within kRsStage and LDS)");
     GemvArgs ga;
     launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, op_gemv_args(ga), waves,
                    (hipStream_t)stream);
@@ -1641,7 +1645,8 @@ int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int3
                      int32_t S, int32_t waves, void* stream) {
   return op_guard([&] {
     REQUIRE(X && W && slabs && N >= 16 && S >= 1, MS_EINVAL, "bad gemv_split operands");
-    REQUIRE(gemv_split_supported(M, N, K, S), MS_EINVAL, "gemv_split shape unsupported (M<=64, (K/S)%64==0)");
+    REQUIRE(gemv_split_supported(M, N, K, S, op_rs_tiles()), MS_EINVAL,
+            "gemv_split shape unsupported (M<=64, (K/S)%64==0, row-scale statistics within kRsStage and LDS)");
     GemvArgs ga;
     launch_gemv_split((const bf16_t*)X, (const bf16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream,
                       op_gemv_args(ga));
@@ -1686,7 +1691,8 @@ int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int3
     REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
     REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0),
             MS_EINVAL, "bad epilogue");
-    REQUIRE(qgemv_supported(M, N, K, epi), MS_EINVAL, "qgemv shape unsupported (M<=64, K%256==0, N%16==0)");
+    REQUIRE(qgemv_supported(M, N, K, epi, op_rs_tiles()), MS_EINVAL,
+            "qgemv shape unsupported (M<=64, K%256==0, N%16==0, row-scale statistics within kRsStage and LDS)");
     QMat q{};
     q.n = 1;
     q.base0 = (const uint8_t*)packed;
@@ -1703,7 +1709,8 @@ int ms_op_qgemv_split(const void* X, int32_t type, const void* packed, float* sl
   return op_guard([&] {
     REQUIRE(X && packed && slabs && N >= 16 && S >= 1, MS_EINVAL, "bad qgemv_split operands");
     REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
-    REQUIRE(qgemv_split_supported(M, N, K, S), MS_EINVAL, "qgemv_split shape unsupported (M<=64, K%(256*S)==0)");
+    REQUIRE(qgemv_split_supported(M, N, K, S, op_rs_tiles()), MS_EINVAL,
+            "qgemv_split shape unsupported (M<=64, K%(256*S)==0, row-scale statistics within kRsStage and LDS)");
     QMat q{};
     q.n = 1;
     q.base0 = (const uint8_t*)packed;

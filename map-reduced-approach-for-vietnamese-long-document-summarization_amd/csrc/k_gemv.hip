@@ -243,14 +243,22 @@ static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N
 #undef GE
 }
 
-bool gemv_supported(int M, int N, int K, int epi) {
+bool gemv_supported(int M, int N, int K, int epi, int rs_tiles) {
   if (M < 1 || M > 64 || K % 64) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
   if (epi == MS_GEMV_EPI_ARGMAX && N % 16) return false;
   const GemvPlan p = gemv_plan(M, N, K, epi);
   if (p.waves == 0) return false;
+  // the residual epilogue's prefetch covers one element per thread of a >= 256-thread block
+  if (epi == MS_GEMV_EPI_RESID_SSQ && p.waves < 4) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && gemv_lds_bytes(p, M, K, true) > kMaxLds) return false;
-  return gemv_lds_bytes(p, M, K, false) <= kMaxLds;
+  RowScale rs{};
+  const bool takes_rs = epi != MS_GEMV_EPI_ARGMAX && epi != MS_GEMV_EPI_ADD_F32 && epi != MS_GEMV_EPI_RESID_SSQ;
+  if (rs_tiles > 0 && takes_rs) {  // gemv_dispatch drops the scale for the other epilogues
+    if (!gemv_rs_supported(M, rs_tiles)) return false;
+    rs = make_row_scale(reinterpret_cast<const float*>(16), rs_tiles, 1, 0.f);
+  }
+  return gemv_lds_bytes(p, M, K, false, rs) <= kMaxLds;
 }
 
 static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
@@ -291,9 +299,9 @@ void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int
 
 bool gemv_rs_supported(int M, int tiles) { return M >= 1 && tiles >= 1 && tiles * M <= kRsStage; }
 
-bool gemv_split_supported(int M, int N, int K, int S) {
+bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles) {
   if (S < 1 || K % S) return false;
-  return gemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32);
+  return gemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32, rs_tiles);
 }
 
 void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,

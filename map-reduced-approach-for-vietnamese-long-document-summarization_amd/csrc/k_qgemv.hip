@@ -396,11 +396,16 @@ static size_t qlds(const QPlan& p, int M, int K, const RowScale& rs = RowScale{}
   return gemv_lds_total(qlds_main(p, M, K), rs, M);
 }
 
-bool qgemv_supported(int M, int N, int K, int epi) {
+bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles) {
   if (M < 1 || M > 64 || K % 256 || N % 16) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
   const QPlan p = qplan(M, N, K, epi);
-  return p.waves > 0 && qlds(p, M, K) <= kLdsCap;
+  RowScale rs{};
+  if (rs_tiles > 0 && epi != MS_GEMV_EPI_ARGMAX && epi != MS_GEMV_EPI_ADD_F32) {  // qgemv_go drops it there
+    if (!gemv_rs_supported(M, rs_tiles)) return false;
+    rs = make_row_scale(reinterpret_cast<const float*>(16), rs_tiles, 1, 0.f);
+  }
+  return p.waves > 0 && qlds(p, M, K, rs) <= kLdsCap;
 }
 
 template <int MT, int NT, int EPI>
@@ -466,9 +471,9 @@ void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K
   }
 }
 
-bool qgemv_split_supported(int M, int N, int K, int S) {
+bool qgemv_split_supported(int M, int N, int K, int S, int rs_tiles) {
   if (S < 1 || K % (256 * S)) return false;
-  return qgemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32);
+  return qgemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32, rs_tiles);
 }
 
 // fp32 partial slabs [S][M][N] over S equal K ranges (super-block aligned); the caller

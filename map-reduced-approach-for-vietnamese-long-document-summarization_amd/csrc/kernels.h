@@ -122,7 +122,7 @@ struct GemvArgs {
 };
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)
-bool gemv_split_supported(int M, int N, int K, int S);
+bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);
 // whether a decode GEMV / Q-GEMV can take a deferred-norm scale of `tiles` partial sums per row
 // (staged in LDS: tiles * M <= 4096)
 bool gemv_rs_supported(int M, int tiles);
@@ -141,7 +141,9 @@ bool residual_rmsnorm_supported(int S, int H);
 void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
                              float* ssq, int rows, int H, hipStream_t s);
 size_t gemv_workspace_bytes(int M, int N, int K);
-bool gemv_supported(int M, int N, int K, int epi);
+// rs_tiles > 0: the call carries deferred-norm statistics of that many tiles (RowScale), which
+// the staged-partials LDS and kRsStage must also fit
+bool gemv_supported(int M, int N, int K, int epi, int rs_tiles = 0);
 void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, void* ws, hipStream_t s);
 // ga: prologue/epilogue arguments (or null); force_waves: tuning hook (0 = heuristic)
@@ -182,8 +184,8 @@ void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t*
                        int map_mul, int map_add, uint8_t* dst_q, int q_row_base, hipStream_t s);
 void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t seed, float scale,
                           hipStream_t s);
-bool qgemv_supported(int M, int N, int K, int epi);
-bool qgemv_split_supported(int M, int N, int K, int S);
+bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles = 0);
+bool qgemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);
 void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
                         hipStream_t s, const GemvArgs* ga = nullptr);
 void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,

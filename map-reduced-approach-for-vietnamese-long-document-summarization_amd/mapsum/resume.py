@@ -54,9 +54,13 @@ class CallJournal:
                     f.truncate(keep)
                     self.torn_lines += 1
                     data = data[:keep]
-            for line in data.decode("utf-8", errors="replace").splitlines():
+            # records end in b"\n" only: str.splitlines() would also split on U+2028/U+2029/
+            # U+0085, which json.dumps(ensure_ascii=False) writes unescaped inside a summary
+            for raw in data.split(b"\n"):
+                if not raw:
+                    continue
                 try:
-                    rec = json.loads(line)
+                    rec = json.loads(raw.decode("utf-8", errors="replace"))
                     self._done[rec["k"]] = rec["text"]
                 except (json.JSONDecodeError, KeyError, TypeError):
                     self.torn_lines += 1

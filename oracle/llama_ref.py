@@ -55,6 +55,30 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32)
 
 
+def _f16(x):
+    """float32 -> nearest-even fp16 (subnormals included), returned as float32."""
+    return np.asarray(x, dtype=np.float32).astype(np.float16).astype(np.float32)
+
+
+def _f16_weights(w: dict) -> dict:
+    """The F16 GGUF of a model: matrices rounded to fp16, norm weights kept fp32 (as
+    llama.cpp's converter stores 1-D tensors)."""
+    out = {k: v for k, v in w.items() if k != "layers"}
+    for k in ("embed", "lm_head"):
+        out[k] = _f16(w[k])
+    if w["lm_head"] is w["embed"]:
+        out["lm_head"] = out["embed"]
+    out["layers"] = [{k: (v if k.endswith("norm") else _f16(v)) for k, v in L.items()}
+                     for L in w["layers"]]
+    return out
+
+
+def rms_rinv_f64(x: np.ndarray, eps: float) -> np.ndarray:
+    """ggml_compute_forward_rms_norm_f32: sum of squares in double, scale = 1/sqrtf(mean + eps)."""
+    ms = (np.sum(x.astype(np.float64) ** 2, axis=-1, keepdims=True) / x.shape[-1]).astype(np.float32)
+    return (np.float32(1.0) / np.sqrt(ms + np.float32(eps))).astype(np.float32)
+
+
 def rms_rinv(x: np.ndarray, eps: float) -> np.ndarray:
     """The RMSNorm factor r = 1/sqrt(mean(x^2) + eps) per row, [..., 1] fp32."""
     ms = np.mean(x.astype(np.float32) ** 2, axis=-1, keepdims=True, dtype=np.float32)
@@ -86,12 +110,29 @@ def silu(x):
 class OracleLlama:
     """Greedy Llama-3.2 over bf16-valued float32 weights (oracle.synth.make_weights layout)."""
 
-    def __init__(self, cfg, weights: dict, round_bf16: bool = True):
-        """round_bf16=False turns every activation rounding off (pure fp32): the mode
-        used to pin this restatement against transformers.LlamaForCausalLM."""
+    MODES = ("bf16", "fp32", "f16")
+
+    def __init__(self, cfg, weights: dict, round_bf16: bool = True, mode: str | None = None):
+        """Numerics mode (``mode`` wins over ``round_bf16``):
+
+        * ``"bf16"`` (default) -- the engine's contract (module docstring, DESIGN.md §2);
+        * ``"fp32"`` (``round_bf16=False``) -- every activation rounding off: un-rounded Llama,
+          the mode pinned against transformers.LlamaForCausalLM;
+        * ``"f16"`` -- ggml's CPU graph for an F16 GGUF, the arithmetic Ollama runs for
+          ``llama3.2:3b-instruct-fp16`` (EXT llama.cpp ``llm_build_llama`` without flash
+          attention, F16 KV cache): weights rounded to fp16 (what the GGUF holds), RMSNorm
+          applied in fp32 before the matmul and its output rounded to fp16 (ggml converts
+          every F32 ``src1`` to the F16 weight's vec_dot type), K and V rounded to fp16 when
+          written to the cache, Q rounded to fp16 for K.Q, the softmax probabilities rounded
+          to fp16 for V.P, the attention output and SwiGLU product rounded to fp16 at their
+          matmuls; fp32 accumulation, fp32 residual, RMSNorm sum of squares in double."""
         self.cfg = cfg
+        self.mode = mode if mode is not None else ("bf16" if round_bf16 else "fp32")
+        assert self.mode in self.MODES, self.mode
+        if self.mode == "f16":
+            weights = _f16_weights(weights)
         self.w = weights
-        self.rnd = bf16_rne if round_bf16 else _f32
+        self.rnd = {"bf16": bf16_rne, "fp32": _f32, "f16": _f16}[self.mode]
 
     def new_cache(self):
         return {"k": [None] * self.cfg.n_layers, "v": [None] * self.cfg.n_layers, "len": 0}
@@ -112,14 +153,24 @@ class OracleLlama:
         G = Hq // Hk
         scale = np.float32(1.0 / math.sqrt(D))
         rnd = self.rnd
+        f16 = self.mode == "f16"
+        eps = cfg.norm_eps
+
+        def normed(x, g):
+            """(GEMM input, per-row factor applied after the GEMM)."""
+            if f16:  # ggml: rms_norm then mul by g in fp32, the matmul rounds its input
+                return _f16((x * rms_rinv_f64(x, eps)) * g), np.float32(1.0)
+            return norm_input(x, g, rnd), rms_rinv(x, eps)
+
+        pre = _f32 if f16 else rnd  # Q/K/V before RoPE: ggml keeps them fp32
         x = w["embed"][ids].astype(np.float32)
         probes = []
         for l, L in enumerate(w["layers"]):
-            xg, r = norm_input(x, L["attn_norm"], rnd), rms_rinv(x, cfg.norm_eps)
-            q = rnd(r * (xg @ L["wq"].T)).reshape(T, Hq, D)
-            k = rnd(r * (xg @ L["wk"].T)).reshape(T, Hk, D)
+            xg, r = normed(x, L["attn_norm"])
+            q = pre(r * (xg @ L["wq"].T)).reshape(T, Hq, D)
+            k = pre(r * (xg @ L["wk"].T)).reshape(T, Hk, D)
             v = rnd(r * (xg @ L["wv"].T)).reshape(T, Hk, D)
-            q = apply_rope(q, cos, sin, rnd)
+            q = apply_rope(q, cos, sin, rnd)  # f16: Q rounded for K.Q, K for the F16 cache
             k = apply_rope(k, cos, sin, rnd)
             if cache["k"][l] is not None:
                 k = np.concatenate([cache["k"][l], k], axis=0)
@@ -134,9 +185,11 @@ class OracleLlama:
             s = s - s.max(axis=-1, keepdims=True)
             p = np.exp(s)
             p = p / p.sum(axis=-1, keepdims=True)
+            if f16:  # V.P: ggml rounds the fp32 probabilities to the F16 V's vec_dot type
+                p = _f16(p)
             o = rnd(np.matmul(p.astype(np.float32), vq.transpose(1, 0, 2)).transpose(1, 0, 2))  # [T, Hq, D]
             x = x + o.reshape(T, Hq * D) @ L["wo"].T
-            xg, r = norm_input(x, L["ffn_norm"], rnd), rms_rinv(x, cfg.norm_eps)
+            xg, r = normed(x, L["ffn_norm"])
             g = r * (xg @ L["w_gate"].T)
             u = r * (xg @ L["w_up"].T)
             h = rnd(silu(g) * u)
@@ -145,7 +198,7 @@ class OracleLlama:
                 probes.append(x.copy())
         cache["len"] = p0 + T
         xs = x if all_logits else x[-1:]
-        xg, r = norm_input(xs, w["final_norm"], rnd), rms_rinv(xs, cfg.norm_eps)
+        xg, r = normed(xs, w["final_norm"])
         logits = r * (xg @ w["lm_head"].T)
         return (logits if all_logits else logits[0]), probes
 

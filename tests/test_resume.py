@@ -66,6 +66,19 @@ def test_journal_roundtrip_and_torn_line(tmp_path):
     j.close()
 
 
+def test_journal_keeps_unicode_line_separators(tmp_path):
+    """json.dumps(ensure_ascii=False) writes U+2028 / U+2029 / U+0085 unescaped: a record that
+    holds one is still one record on reload (str.splitlines() tore it)."""
+    p = tmp_path / "calls.jsonl"
+    text = "dòng một\u2028dòng hai\u2029ba\x85bốn"
+    with CallJournal(str(p)) as j:
+        j.put("k1", "d", text)
+        j.put("k2", "d", "hai")
+    j = CallJournal(str(p))
+    assert len(j) == 2 and j.get("k1") == text and j.torn_lines == 0
+    j.close()
+
+
 def test_crashed_map_phase_resumes_to_the_same_result(tmp_path):
     contents = _contents()
     want = mr.run_map_reduce(FakeLLM(), contents, token_max=40)
