@@ -32,7 +32,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "map-phase chunks/sec (2k-tok chunk, 256-tok summary) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
-BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA (MI355X_MICROARCH.md chip table)
+F16_PEAK_TFLOPS = 2500.0    # dense fp16 (= bf16) MFMA (MI355X_MICROARCH.md chip table)
 CHUNKS_PER_DOC = 8          # BASELINE.json configs[0..2]: a 16k-token doc in 2k chunks
 
 
@@ -93,7 +93,7 @@ def lm_head_bytes_per_step(cfg, B, quant=False):
 
 def decode_weight_bytes(cfg, quant=False):
     """Weight bytes one decode step streams (every layer matrix + the lm_head): SURVEY.md
-    §8d's W = 6,425,149,440 B for bf16 Llama-3.2-3B."""
+    §8d's W = 6,425,149,440 B for 16-bit Llama-3.2-3B (the engine holds fp16)."""
     if not quant:
         return cfg.weight_bytes
     return qgemv_bytes_per_step(cfg, 0) + cfg.vocab * cfg.hidden * 224 / 256
@@ -107,22 +107,43 @@ def prefill_flops_per_chunk(cfg, P):
     return 2 * lin * P + 2 * cfg.vocab * H + attn
 
 
-def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=16):
+def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=64):
     """BASELINE.md §2 fallback (Ollama and the GGUF are absent on the box): the torch-CPU
     bf16 restatement of the same map call (oracle/torch_cpu.py), all 28 layers, on one
     chunk of this workload: its full 2048-token prefill + ``decode_sample`` greedy decode
-    steps, extrapolated to the 256 generated tokens."""
+    steps, extrapolated to the 256 generated tokens.  Threads: every CPU this process may
+    run on (its affinity mask -- BASELINE.md §2 asks for num_thread = physical cores; the
+    sample text records both counts)."""
     import torch
     from oracle.torch_cpu import time_chunk
+    allowed = len(os.sched_getaffinity(0))
+    torch.set_num_threads(allowed)
+    phys = _physical_cores()
     r = time_chunk(cfg, prompt_ids, gen_len, decode_sample=decode_sample)
     return {"value": round(1.0 / r["chunk_s"], 5), "unit": "chunks/s", "cores": int(r["threads"]),
             "kind": "port", "cpu_model": r["cpu_model"],
             "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16 on {r['cpu_model']}, "
+                       f"{r['threads']} threads = every CPU of this process's affinity mask ({allowed}; "
+                       f"{phys} physical cores on the host), "
                        f"{cfg.n_layers}-layer Llama-3.2-3B on the engine's own synthetic weights, "
                        f"1 chunk: {len(prompt_ids)}-tok prefill "
                        f"{r['prefill_s']:.2f} s + {r['decode_steps_timed']} decode steps at "
                        f"{r['decode_step_s'] * 1e3:.1f} ms, extrapolated to {gen_len} tokens "
                        f"({r['chunk_s']:.1f} s/chunk)")}
+
+
+def _physical_cores():
+    """Distinct (physical id, core id) pairs in /proc/cpuinfo (None if unreadable)."""
+    try:
+        cores, phys = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":")[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":")[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
 
 
 def pmc_traffic(weights, B, prompt_len):
@@ -166,7 +187,7 @@ def parse_args(argv=None):
     ap.add_argument("--prompt-len", type=int, default=2048)
     ap.add_argument("--gen-len", type=int, default=256)
     ap.add_argument("--model", default="llama3.2-3b")
-    ap.add_argument("--weights", choices=("bf16", "q4_k_m"), default="bf16",
+    ap.add_argument("--weights", choices=("f16", "q4_k_m"), default="f16",
                     help="q4_k_m = BASELINE configs[4]: random Q4_K/Q6_K blocks, K-quant decode GEMVs")
     ap.add_argument("--eos", type=int, default=0,
                     help="natural-EOS mode: stop at a synthetic set of N stop ids (seeded) instead of "
@@ -305,7 +326,7 @@ def main():
             traffic, traffic_src = pmc_traffic(args.weights, B, args.prompt_len)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (bf16")
+                    "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (fp16")
                               + " decode weight stream: QKV/O/gate-up/down projections + lm_head)",
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
@@ -317,8 +338,8 @@ def main():
     dec_bytes = (st["decode_steps"] * decode_weight_bytes(cfg, quant) + st["decode_kv_tokens"] * kvb
                  + st["decode_tokens"] * kvb)
     dec_gbs = dec_bytes / (st["decode_ms"] / 1e3) / 1e9 if st["decode_ms"] else None
-    roof_pre = {"bound": "mfma", "achieved": round(pre_tf, 1), "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(pre_tf / BF16_PEAK_TFLOPS, 4),
+    roof_pre = {"bound": "mfma", "achieved": round(pre_tf, 1), "peak": F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(pre_tf / F16_PEAK_TFLOPS, 4),
                 "flops_per_chunk": prefill_flops_per_chunk(cfg, args.prompt_len),
                 "method": "SURVEY.md §8d prefill FLOP / event-timed prefill passes (all kernels)"} if pre_tf else None
     roof_dec = {"bound": "hbm", "achieved": round(dec_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -330,9 +351,9 @@ def main():
         "metric": METRIC, "value": round(value, 4), "unit": "chunks/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 2),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "q4_k_m+bf16" if quant else "bf16",
+        "dtype": "q4_k_m+f16" if quant else "f16",
         "data": ("synthetic (random Q4_K/Q6_K blocks in the Q4_K_M mix, seed 2, uniform token ids)"
-                 if quant else "synthetic (random-init Llama-3.2-3B bf16 weights, uniform token ids)"),
+                 if quant else "synthetic (random-init Llama-3.2-3B weights held as fp16, uniform token ids)"),
         "config": {"workload": (f"configs[2]: {args.docs} docs x {CHUNKS_PER_DOC} x {args.prompt_len}-tok "
                                 f"chunks over {world} GPU(s) ({n_local} per GPU, <= {B} in flight, "
                                 f"continuous batching)" if args.docs else

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define MS_ABI_VERSION 2
+#define MS_ABI_VERSION 3  /* 3: the 16-bit type is IEEE fp16 (weights, KV cache, activations) */
 
 /* status codes */
 #define MS_OK 0
@@ -56,7 +56,7 @@ extern "C" {
 /* ms_submit flags */
 #define MS_FLAG_IGNORE_EOS 1u /* bench mode: always generate num_predict tokens */
 
-/* logical weight tensors for ms_load_weight ([rows][cols] row-major bf16, HF
+/* logical weight tensors for ms_load_weight ([rows][cols] row-major fp16, HF
  * nn.Linear layout [out][in]); the engine fuses Q|K|V and interleaves gate/up
  * on upload. */
 enum ms_tensor {
@@ -126,15 +126,15 @@ int ms_destroy(ms_engine* e);
 const char* ms_last_error(const ms_engine* e);
 
 /* ---- weights ---------------------------------------------------------------- */
-int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host_bf16,
+int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* host_f16,
                    int64_t n_elems);
 /* device-side counter-based N(0,std)-like init; restated in oracle/synth.py */
 int ms_init_synthetic(ms_engine* e, uint64_t seed, float std, float norm_jitter);
 
 /* ggml K-quant weights (Q4_K_M files: BASELINE.json config 5).  `blocks` are the tensor's
  * rows as raw ggml blocks (Q4_K = 144 B, Q6_K = 210 B per 256 weights).  The engine keeps
- * bf16(dequant) for prefill and the blocks for the dequant-fused decode GEMV.  RMSNorm
- * weights stay bf16 (ms_load_weight). */
+ * f16(dequant) for prefill and the blocks for the dequant-fused decode GEMV.  RMSNorm
+ * weights stay fp16 (ms_load_weight). */
 #define MS_GGML_Q4_K 12
 #define MS_GGML_Q6_K 14
 int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggml_type,
@@ -143,7 +143,7 @@ int ms_load_weight_q(ms_engine* e, int32_t tensor, int32_t layer, int32_t ggml_t
 int ms_init_synthetic_q(ms_engine* e, uint64_t seed, float scale, float norm_jitter);
 
 /* ---- weight broadcast (one process per GPU: rank 0 loads, the others receive over RCCL) -- */
-/* every device weight buffer in a fixed order (bf16 matrices and norms, then K-quant
+/* every device weight buffer in a fixed order (fp16 matrices and norms, then K-quant
    regions); returns the count, fills up to cap (ptr, bytes) pairs */
 int ms_weight_regions(const ms_engine* e, void** ptrs, int64_t* bytes, int32_t cap);
 /* the (tensor, layer, ggml_type) triples of the K-quant tensors loaded so far; returns the count */
@@ -194,9 +194,9 @@ int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t*
                      int32_t n_forced, int32_t num_predict, uint32_t flags, uint64_t tag);
 
 /* ---- op-level entry points (device pointers; stream = hipStream_t or NULL) -- */
-#define MS_EPI_STORE_BF16 0  /* out bf16 [M][ldo]                              */
+#define MS_EPI_STORE_F16 0  /* out fp16 [M][ldo]                              */
 #define MS_EPI_ADD_F32 1     /* out fp32 [M][ldo] += acc  (residual add)       */
-#define MS_EPI_SWIGLU 2      /* W rows interleaved gate/up per 16; out bf16 [M][N/2] */
+#define MS_EPI_SWIGLU 2      /* W rows interleaved gate/up per 16; out fp16 [M][N/2] */
 #define MS_EPI_STORE_F32 3   /* out fp32 [M][ldo]                              */
 #define MS_EPI_ARGMAX 5      /* decode GEMV only: out {max, id} float2 [M][ldo = N/16], one per
                                 16-column tile (ties -> lowest id; NaN never wins); finish the
@@ -218,7 +218,7 @@ int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32
                        int32_t ldk, int32_t ldo, int32_t epilogue, void* stream);
 /* decode O / down with the residual update fused (the engine's small-regime layer): x fp32
    [M][N] += X . W^T on rt-row tiles (N % rt == 0, tiles = N / rt <= 256), and the input of the
-   next normalised projection: xg_out bf16 [M][N] = bf16(x * gamma), ssq_out fp32 [tiles][M] =
+   next normalised projection: xg_out fp16 [M][N] = f16(x * gamma), ssq_out fp32 [tiles][M] =
    per-tile sums of the new x^2 (its deferred RMSNorm statistics, see ms_op_set_row_scale) */
 int ms_op_gemv_resid(const void* X, const void* W, float* x, void* xg_out, const void* gamma,
                      float* ssq_out, int32_t M, int32_t N, int32_t K, int32_t rt, void* stream);
@@ -238,14 +238,14 @@ int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, i
 int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
                      int32_t S, int32_t waves, void* stream);
 /* x fp32 [rows][hidden] += slab_0 + ... + slab_{S-1} (slab order); then the input of the
-   normalised projection that follows: y bf16 = bf16(x * w), ssq[r] = sum of x[r]^2 (one tile) */
+   normalised projection that follows: y fp16 = f16(x * w), ssq[r] = sum of x[r]^2 (one tile) */
 int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y, float* ssq,
                            int32_t rows, int32_t hidden, void* stream);
 /* K-quant ops: raw ggml blocks -> fp32 (bit-exact restatement of llama.cpp's
-   dequantize_row_q4_K/q6_K); raw rows -> bf16 rows + packed rows (Q6_K repacked to 224 B);
+   dequantize_row_q4_K/q6_K); raw rows -> fp16 rows + packed rows (Q6_K repacked to 224 B);
    dequant-fused GEMV over packed rows (same epilogues as ms_op_gemv) */
 int ms_op_dequant(int32_t ggml_type, const void* blocks, int64_t n_blocks, float* out, void* stream);
-int ms_op_quant_rows(int32_t ggml_type, const void* blocks, int32_t rows, int32_t K, void* bf16_out,
+int ms_op_quant_rows(int32_t ggml_type, const void* blocks, int32_t rows, int32_t K, void* f16_out,
                      void* packed_out, void* stream);
 int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void* out, int32_t M,
                 int32_t N, int32_t K, int32_t ldo, int32_t epilogue, void* stream);
@@ -253,7 +253,7 @@ int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void*
    (the quantised counterpart of ms_op_gemv_split; K % (256*S) == 0) */
 int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows, float* slabs,
                       int32_t M, int32_t N, int32_t K, int32_t S, void* stream);
-/* the input of a normalised projection: y bf16 [rows][hidden] = bf16(x * w) and ssq[r] = sum
+/* the input of a normalised projection: y fp16 [rows][hidden] = f16(x * w) and ssq[r] = sum
    of x[r]^2 over x fp32 [.][hidden] rows (row_idx optional gather); the projection then scales
    its output rows by 1/sqrt(ssq / hidden + eps) (ms_op_set_row_scale) */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, float* ssq, int32_t rows, int32_t hidden,

@@ -4,9 +4,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-typedef uint16_t bf16_t;  // storage type for bf16 in HBM
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+// The engine's 16-bit type is IEEE fp16 (numerics contract): the
+// reference runs llama3.2:3b-instruct-fp16 on ggml's F16 path, and fp16 carries three more
+// mantissa bits than bf16 at the same MFMA rate on gfx950 (v_mfma_f32_16x16x32_f16).
+typedef uint16_t f16_t;  // storage type for fp16 in HBM
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 
@@ -37,26 +41,24 @@ constexpr int kWave = 64;
 constexpr int kHeadDim = 128;
 constexpr int kPage = 64;  // KV page = 64 tokens = one attention K/V tile
 
-__device__ __forceinline__ float bf2f(bf16_t u) { return __uint_as_float((uint32_t)u << 16); }
+__device__ __forceinline__ float h2f(f16_t u) { return (float)__builtin_bit_cast(_Float16, u); }
+// the two fp16 halves of a packed word (low element first, as stored in memory)
+__device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(f16x2, w)[0]; }
+__device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(f16x2, w)[1]; }
 
-// round-to-nearest-even; hipcc lowers the __bf16 cast to v_cvt_pk_bf16_f32 (NaN-safe)
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  __bf16 b = (__bf16)f;
-  return __builtin_bit_cast(bf16_t, b);
-}
+// round-to-nearest-even (v_cvt_f16_f32; overflow -> inf, NaN stays NaN)
+__device__ __forceinline__ f16_t f2h(float f) { return __builtin_bit_cast(f16_t, (_Float16)f); }
 
-// one v_cvt_pk_bf16_f32 for the pair (same RNE rounding as f2bf): packing two f2bf results
-// by shift + or compiled to two converts, a shift and an sdwa or
-__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+// one v_cvt_pk_f16_f32 for the pair (same RNE rounding as f2h)
+__device__ __forceinline__ uint32_t pack2h(float lo, float hi) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b2 __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){lo, hi}, b2));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){lo, hi}, f16x2));
 }
 
-__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+__device__ __forceinline__ f16x8 as_f16x8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
 
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

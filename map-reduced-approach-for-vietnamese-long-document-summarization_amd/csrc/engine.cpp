@@ -11,8 +11,8 @@
 //             -> one packed varlen prefill pass over all admitted prompts
 //             -> one decode step for every running sequence.
 // Device memory is laid out once at ms_create for the configured max batch:
-// bf16 weights (Q|K|V fused, gate/up interleaved per 16 rows), a paged bf16 KV
-// pool [layer][page][kv_head][64][128], fp32 residual stream, bf16 activations.
+// fp16 weights (Q|K|V fused, gate/up interleaved per 16 rows), a paged fp16 KV
+// pool [layer][page][kv_head][64][128], fp32 residual stream, fp16 activations.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -75,7 +75,7 @@ struct Seq {
 };
 
 struct Layer {
-  bf16_t *attn_norm = nullptr, *wqkv = nullptr, *wo = nullptr, *ffn_norm = nullptr,
+  f16_t *attn_norm = nullptr, *wqkv = nullptr, *wo = nullptr, *ffn_norm = nullptr,
          *wgu = nullptr, *wdown = nullptr;
 };
 
@@ -102,16 +102,16 @@ struct ms_engine {
   std::vector<Layer> layers;
   std::vector<std::array<QSlot, 4>> lq;  // per layer: QKV, O, gate/up, down
   QSlot lmq;                             // lm_head (the tied embedding when tie_embeddings)
-  bf16_t *embed = nullptr, *final_norm = nullptr, *lm_head = nullptr;
+  f16_t *embed = nullptr, *final_norm = nullptr, *lm_head = nullptr;
   float *cos_tab = nullptr, *sin_tab = nullptr;
-  bf16_t *kpool = nullptr, *vpool = nullptr;
+  f16_t *kpool = nullptr, *vpool = nullptr;
   size_t layer_kv_elems = 0;
   int32_t* bt_d = nullptr;
   int32_t* bt_h = nullptr;  // pinned host copy of the block table (async row uploads)
   std::vector<int> free_pages, free_slots;
   float* x = nullptr;
   float* ssq = nullptr;
-  bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
+  f16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
   float* logits = nullptr;
   int32_t* ids_out_d = nullptr;
   void* gemv_ws = nullptr;
@@ -130,9 +130,9 @@ struct ms_engine {
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
-  // Residual-fused decode (small-regime engines, bf16 O / down): O and down run unsplit on
+  // Residual-fused decode (small-regime engines, fp16 O / down): O and down run unsplit on
   // resid_rt-row tiles (3072 / 12 = 256 workgroups, one per CU) and their epilogue adds into
-  // the fp32 residual and emits the next projection's input itself -- xb = bf16(x * g_next)
+  // the fp32 residual and emits the next projection's input itself -- xb = f16(x * g_next)
   // and per-tile sums of x^2 (ssq [256][B]) -- so the decode layer has no residual_rmsnorm
   // launch: the deferred RMSNorm (kernels.h RowScale) scales the rows of the QKV / gate-up /
   // lm_head outputs instead.  Chosen per engine (MS_RESID_FUSED=0: split-K slabs + norm
@@ -145,8 +145,8 @@ struct ms_engine {
     return resid_fuse && !large_engine && !(q && q->ready());
   }
   bool large(int) const { return large_engine; }
-  // split count of every quantised slab projection (MS_QSPLIT; 0: as bf16): 4 measured best
-  // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the bf16 splits (6 / 6 / 4), 2 / 3 / 8
+  // split count of every quantised slab projection (MS_QSPLIT; 0: as fp16): 4 measured best
+  // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the fp16 splits (6 / 6 / 4), 2 / 3 / 8
   // slower (profiles/r02/v27_qsplit_sweep_q4_k_m.txt)
   int qsplit = 4;
   // decode attention variant (tuning): q/k/v from QKV split slabs (else the GEMV RoPE
@@ -172,7 +172,7 @@ struct ms_engine {
     hipStream_t stream = nullptr;
     float* x = nullptr;
     float* ssq = nullptr;  // sums of x^2 behind xb: [rows] (norm kernels) or [256][rows] (RESID)
-    bf16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
+    f16_t *xb = nullptr, *qkv = nullptr, *attn = nullptr, *hbuf = nullptr;
     float* logits = nullptr;
     int32_t* ids_out_d = nullptr;
     int32_t* args_d = nullptr;
@@ -275,7 +275,7 @@ struct ms_engine {
   RowScale norm_rs() const { return make_row_scale(ssq, 1, H, cfg.norm_eps); }
 
   // normalised (rs) or plain projection: the decode GEMV where it fits, else the MFMA GEMM
-  void gemm_or_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+  void gemm_or_gemv(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, bool decode, int cls, const RowScale* rs = nullptr) {
     prof_begin(cls);
     if (decode && gemv_supported(M, N, K, epi)) {
@@ -289,7 +289,7 @@ struct ms_engine {
   }
 
   // decode projection: the K-quant stream when that matrix was loaded quantised
-  void proj(const QSlot* q, const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K,
+  void proj(const QSlot* q, const f16_t* X, const f16_t* W, void* out, int M, int N, int K,
             int ldo, int epi, const GemvArgs* ga, int cls) {
     prof_begin(cls);
     if (q && q->ready() && qgemv_supported(M, N, K, epi))
@@ -322,17 +322,17 @@ struct ms_engine {
 
   // normalised projection into fp32 partial slabs [S][M][N], rows scaled by cur_rs; returns
   // the number of slabs written
-  int proj_split(const QSlot* q, const bf16_t* X, const bf16_t* W, int M, int N, int K, int S, int Sl,
+  int proj_split(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
                  const RowScale* rs) {
     prof_begin(K_GEMV);
     GemvArgs ga{};
     if (rs) ga.rs = *rs;
     int used = 1;
-    if (large(M)) {  // skinny GEMM on the bf16 weights (K-quant copies included)
+    if (large(M)) {  // skinny GEMM on the fp16 weights (K-quant copies included)
       launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
       used = Sl;
     } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
-      // Q4_K/Q6_K: same split-K as bf16 (a 16-row tile carries 3.6x fewer weight bytes, so
+      // Q4_K/Q6_K: same split-K as fp16 (a 16-row tile carries 3.6x fewer weight bytes, so
       // the unsplit grid -- 192 blocks for O/down -- is too thin to cover 256 CUs)
       const int Sq = qsplit > 0 ? qsplit : S;
       if (Sq > 1 && Sq <= kMaxSplit && qgemv_split_supported(M, N, K, Sq)) {
@@ -350,8 +350,8 @@ struct ms_engine {
     return used;
   }
 
-  // fold pending slabs into x, then xb = bf16(x * w) and its one-tile statistics
-  void residual_norm(const bf16_t* w, int B) {
+  // fold pending slabs into x, then xb = f16(x * w) and its one-tile statistics
+  void residual_norm(const f16_t* w, int B) {
     prof_begin(K_MISC);
     launch_residual_rmsnorm(x, slabs, pending_split, w, xb, ssq, B, H, stream);
     prof_end(K_MISC);
@@ -362,8 +362,8 @@ struct ms_engine {
   // the residual update of O / down: x += X . W^T, then the input of the next normalised
   // projection (gain g_next) -- in the GEMV epilogue (resid_fused: RESID_SSQ on resid_rt-row
   // tiles, 256 tiles of statistics) or as split-K slabs + one residual_rmsnorm launch
-  void resid_update(const QSlot* q, const bf16_t* X, const bf16_t* W, int B, int K, int S, int Sl,
-                    const bf16_t* g_next) {
+  void resid_update(const QSlot* q, const f16_t* X, const f16_t* W, int B, int K, int S, int Sl,
+                    const f16_t* g_next) {
     if (resid_fused(q)) {
       GemvArgs ga{};
       ga.rt = resid_rt;
@@ -423,12 +423,12 @@ struct ms_engine {
       gg.rs = rs_ffn;
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV);
     }
-    const bf16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
+    const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
     resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next);
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each); on entry
-  // xb = bf16(x * attn_norm) with cur_rs, on exit xb = bf16(x * g_next) with cur_rs
+  // xb = f16(x * attn_norm) with cur_rs, on exit xb = f16(x * g_next) with cur_rs
   // (tail = false: the last layer of a prefill whose caller normalises only the rows it needs)
   void run_layer(int l, int T, bool decode, const int32_t* tok_pos, const int32_t* tok_slot,
                  const PrefillAttnArgs& pa, const DecodeAttnArgs& da, bool tail = true) {
@@ -439,7 +439,7 @@ struct ms_engine {
     const Layer& Ly = layers[l];
     const int kc = decode ? K_GEMV : K_GEMM;
     const RowScale rs_attn = cur_rs;
-    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_BF16, decode, kc, &rs_attn);
+    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
     KVView kv = kv_layer(l);
     prof_begin(K_MISC);
     launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
@@ -461,8 +461,8 @@ struct ms_engine {
     if (tail) norm_input(l + 1 < L ? layers[l + 1].attn_norm : final_norm, T);
   }
 
-  // xb = bf16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
-  void norm_input(const bf16_t* w, int T, const int32_t* row_idx = nullptr) {
+  // xb = f16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
+  void norm_input(const f16_t* w, int T, const int32_t* row_idx = nullptr) {
     prof_begin(K_MISC);
     launch_rmsnorm(x, w, xb, ssq, T, H, row_idx, stream);
     prof_end(K_MISC);
@@ -477,7 +477,7 @@ struct ms_engine {
       if (q[0] == tensor && q[1] == layer) { q[2] = type; return; }
     quant_manifest.push_back({tensor, layer, type});
   }
-  // every device weight buffer, in a fixed order: bf16 matrices and norms, then the K-quant
+  // every device weight buffer, in a fixed order: fp16 matrices and norms, then the K-quant
   // regions (the payload of a weight broadcast, dist.broadcast_engine_weights)
   std::vector<std::pair<void*, size_t>> weight_regions() const {
     std::vector<std::pair<void*, size_t>> r;
@@ -504,7 +504,7 @@ struct ms_engine {
     return r;
   }
 
-  // Captured decode graphs bake in the weight form (bf16 vs K-quant stream) and the split
+  // Captured decode graphs bake in the weight form (fp16 vs K-quant stream) and the split
   // choices: any weight (re)load invalidates them.
   void drop_graphs() {
     for (auto& kv : decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
@@ -626,18 +626,18 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.slot_major = E.n_pages == cfg->max_batch * E.max_pages && !getenv("MS_KV_PAGED");
     E.Tmax = std::max(cfg->max_prefill_tokens, cfg->max_batch);
     // weights
-    E.embed = E.dalloc<bf16_t>((size_t)E.V * E.H);
-    E.lm_head = cfg->tie_embeddings ? E.embed : E.dalloc<bf16_t>((size_t)E.V * E.H);
-    E.final_norm = E.dalloc<bf16_t>(E.H);
+    E.embed = E.dalloc<f16_t>((size_t)E.V * E.H);
+    E.lm_head = cfg->tie_embeddings ? E.embed : E.dalloc<f16_t>((size_t)E.V * E.H);
+    E.final_norm = E.dalloc<f16_t>(E.H);
     E.layers.resize(E.L);
     E.lq.resize(E.L);
     for (auto& Ly : E.layers) {
-      Ly.attn_norm = E.dalloc<bf16_t>(E.H);
-      Ly.ffn_norm = E.dalloc<bf16_t>(E.H);
-      Ly.wqkv = E.dalloc<bf16_t>((size_t)E.QKVN * E.H);
-      Ly.wo = E.dalloc<bf16_t>((size_t)E.H * E.Hq * E.D);
-      Ly.wgu = E.dalloc<bf16_t>((size_t)2 * E.F * E.H);
-      Ly.wdown = E.dalloc<bf16_t>((size_t)E.H * E.F);
+      Ly.attn_norm = E.dalloc<f16_t>(E.H);
+      Ly.ffn_norm = E.dalloc<f16_t>(E.H);
+      Ly.wqkv = E.dalloc<f16_t>((size_t)E.QKVN * E.H);
+      Ly.wo = E.dalloc<f16_t>((size_t)E.H * E.Hq * E.D);
+      Ly.wgu = E.dalloc<f16_t>((size_t)2 * E.F * E.H);
+      Ly.wdown = E.dalloc<f16_t>((size_t)E.H * E.F);
     }
     // rope tables
     std::vector<float> cs, sn;
@@ -648,8 +648,8 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     HIP_OK(hipMemcpy(E.sin_tab, sn.data(), sn.size() * 4, hipMemcpyHostToDevice));
     // paged KV pool (zeroed: stale-page bytes are always finite)
     E.layer_kv_elems = (size_t)E.n_pages * E.Hk * kPage * E.D;
-    E.kpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
-    E.vpool = E.dalloc<bf16_t>(E.layer_kv_elems * E.L, true);
+    E.kpool = E.dalloc<f16_t>(E.layer_kv_elems * E.L, true);
+    E.vpool = E.dalloc<f16_t>(E.layer_kv_elems * E.L, true);
     HIP_OK(hipHostMalloc((void**)&E.bt_h, (size_t)cfg->max_batch * E.max_pages * sizeof(int32_t),
                          hipHostMallocDefault));
     std::memset(E.bt_h, 0, (size_t)cfg->max_batch * E.max_pages * sizeof(int32_t));
@@ -662,10 +662,10 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
       const size_t R = c == &E.cp ? T : (size_t)cfg->max_batch;
       c->x = E.dalloc<float>(R * E.H);
       c->ssq = E.dalloc<float>(std::max(R, (size_t)256 * cfg->max_batch), true);
-      c->xb = E.dalloc<bf16_t>(R * E.H);
-      c->qkv = E.dalloc<bf16_t>(R * E.QKVN);
-      c->attn = E.dalloc<bf16_t>(R * E.Hq * E.D);
-      c->hbuf = E.dalloc<bf16_t>(R * E.F);
+      c->xb = E.dalloc<f16_t>(R * E.H);
+      c->qkv = E.dalloc<f16_t>(R * E.QKVN);
+      c->attn = E.dalloc<f16_t>(R * E.Hq * E.D);
+      c->hbuf = E.dalloc<f16_t>(R * E.F);
       c->logits = E.dalloc<float>((size_t)cfg->max_batch * E.V);
       c->ids_out_d = E.dalloc<int32_t>(cfg->max_batch);
     }
@@ -747,9 +747,9 @@ const char* ms_last_error(const ms_engine* e) {
   return g_last_error.c_str();
 }
 
-// where a logical tensor lives: fused bf16 destination + row map, and its K-quant slot
+// where a logical tensor lives: fused fp16 destination + row map, and its K-quant slot
 struct TensorDst {
-  bf16_t* dst = nullptr;
+  f16_t* dst = nullptr;
   int rows = 0, cols = 0, mul = 16, add = 0;
   QSlot* qs = nullptr;
   int qbit = 0, qneed = 0, qregion = 0, qrow0 = 0, qrows = 0;
@@ -809,7 +809,7 @@ int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* 
     REQUIRE(n == (int64_t)t.rows * t.cols, MS_EINVAL,
             "tensor " + std::to_string(tensor) + ": expected " + std::to_string((int64_t)t.rows * t.cols) +
                 " elements, got " + std::to_string(n));
-    if (t.qs) t.qs->loaded &= ~(uint32_t)t.qbit;  // a bf16 reload supersedes a quantised copy
+    if (t.qs) t.qs->loaded &= ~(uint32_t)t.qbit;  // a fp16 reload supersedes a quantised copy
     if (t.rows == 1) {
       HIP_OK(hipMemcpy(t.dst, host, (size_t)n * 2, hipMemcpyHostToDevice));
       return MS_OK;
@@ -818,7 +818,7 @@ int ms_load_weight(ms_engine* e, int32_t tensor, int32_t layer, const uint16_t* 
     HIP_OK(hipMalloc(&tmp, (size_t)n * 2));
     hipError_t ce = hipMemcpy(tmp, host, (size_t)n * 2, hipMemcpyHostToDevice);
     if (ce == hipSuccess) {
-      launch_scatter_rows((const bf16_t*)tmp, t.dst, t.rows, t.cols, t.mul, t.add, E.stream);
+      launch_scatter_rows((const f16_t*)tmp, t.dst, t.rows, t.cols, t.mul, t.add, E.stream);
       ce = hipStreamSynchronize(E.stream);
     }
     (void)hipFree(tmp);
@@ -844,12 +844,12 @@ static uint8_t* q_region(ms_engine& E, QSlot& s, int idx, int row0, int rows, in
   return p;
 }
 
-// device-resident raw ggml blocks of one logical tensor -> bf16 copy + quantised copy
+// device-resident raw ggml blocks of one logical tensor -> fp16 copy + quantised copy
 static void load_quant(ms_engine& E, int tensor, int layer, int type, const uint8_t* dblocks) {
   TensorDst t = tensor_dst(E, tensor, layer);
   REQUIRE(t.rows > 1, MS_EINVAL, "RMSNorm weights are not quantised");
   REQUIRE(t.cols % 256 == 0, MS_EINVAL, "K-quant tensors need cols % 256 == 0");
-  // an untied embedding is only gathered: its bf16 copy is all decode needs
+  // an untied embedding is only gathered: its fp16 copy is all decode needs
   uint8_t* q = t.qs ? q_region(E, *t.qs, t.qregion, t.qrow0, t.qrows, type, t.cols) : nullptr;
   launch_quant_rows(type, dblocks, t.rows, t.cols, t.dst, t.mul, t.add, q, t.qrow0, E.stream);
   HIP_OK(hipGetLastError());
@@ -1164,7 +1164,8 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   std::vector<std::pair<int, int32_t>> qb;
   for (int i = 0; i < S; ++i) {
     const int n = (int)batch[i]->prompt.size();
-    for (int b = 0; b < (n + 63) / 64; ++b) qb.push_back({batch[i]->len + b * 64, (i << 16) | b});
+    for (int b = 0; b < (n + kPrefillQRows - 1) / kPrefillQRows; ++b)
+      qb.push_back({batch[i]->len + b * kPrefillQRows, (i << 16) | b});
   }
   std::stable_sort(qb.begin(), qb.end(), [](auto& x, auto& y) { return x.first > y.first; });
   const size_t o_qblk = a.size();
@@ -1189,7 +1190,7 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   HIP_OK(hipGetLastError());
   if (n_layers_run < E.L) return;
   if (!logits_all && !first_ids) return;  // probe of the final residual only
-  if (logits_all) {  // probe: logits of every position (xb = bf16(x * final_norm), cur_rs)
+  if (logits_all) {  // probe: logits of every position (xb = f16(x * final_norm), cur_rs)
     launch_gemm(E.xb, E.lm_head, logits_all, T, E.V, E.H, E.V, MS_EPI_STORE_F32, E.stream, &E.cur_rs);
     return;
   }
@@ -1221,7 +1222,7 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   E.prof_end(K_MISC);
   E.pending_split = 0;
   E.cur_rs = E.norm_rs();
-  // every layer leaves xb = bf16(x * the next gain) with its deferred scale in cur_rs
+  // every layer leaves xb = f16(x * the next gain) with its deferred scale in cur_rs
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   const RowScale rs = E.cur_rs;
   if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX)) {
@@ -1366,7 +1367,7 @@ int ms_step(ms_engine* e) {
     if (E.large_engine && E.has_quant && !E.warned_quant_large) {
       // say so instead of silently changing arithmetic with the engine size
       fprintf(stderr, "libmapsum: a %d-slot engine decodes in the large-batch regime: K-quant matrices are "
-              "multiplied from their bf16 dequantised copies (skinny MFMA GEMM); the exact fp32 K-quant GEMV "
+              "multiplied from their fp16 dequantised copies (skinny MFMA GEMM); the exact fp32 K-quant GEMV "
               "runs in engines of < %d slots\n", E.cfg.max_batch, E.dgemm_min);
       E.warned_quant_large = true;
     }
@@ -1568,7 +1569,7 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
     REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "gemm row scale: one-tile statistics only");
-    launch_gemm((const bf16_t*)A, (const bf16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
+    launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }
 
@@ -1598,7 +1599,7 @@ int ms_op_gemv_tuned(const void* X, const void* W, void* out, int32_t M, int32_t
             "gemv shape unsupported (M<=64, K%64==0, K/64 split into <=16 waves of <=8 steps; "
             "row-scale statistics within kRsStage and LDS)");
     GemvArgs ga;
-    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldo, epi, op_gemv_args(ga), waves,
+    launch_gemv_ex((const f16_t*)X, (const f16_t*)W, out, M, N, K, ldo, epi, op_gemv_args(ga), waves,
                    (hipStream_t)stream);
   });
 }
@@ -1610,7 +1611,7 @@ int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32
             "bad strided gemv operands");
     REQUIRE(epi >= 0 && epi <= 3 && epi != MS_EPI_SWIGLU, MS_EINVAL, "bad epilogue");
     REQUIRE(gemv_supported(M, N, K, epi), MS_EINVAL, "gemv shape unsupported");
-    launch_gemv_strided((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, ldk, ldo, epi, (hipStream_t)stream);
+    launch_gemv_strided((const f16_t*)X, (const f16_t*)W, out, M, N, K, ldk, ldo, epi, (hipStream_t)stream);
   });
 }
 
@@ -1623,9 +1624,9 @@ int ms_op_gemv_resid(const void* X, const void* W, float* x, void* xg_out, const
     GemvArgs ga{};
     ga.rt = rt;
     ga.ssq_out = ssq_out;
-    ga.gamma = (const bf16_t*)gamma;
-    ga.xg_out = (bf16_t*)xg_out;
-    launch_gemv_ex((const bf16_t*)X, (const bf16_t*)W, x, M, N, K, N, MS_GEMV_EPI_RESID_SSQ, &ga, 0,
+    ga.gamma = (const f16_t*)gamma;
+    ga.xg_out = (f16_t*)xg_out;
+    launch_gemv_ex((const f16_t*)X, (const f16_t*)W, x, M, N, K, N, MS_GEMV_EPI_RESID_SSQ, &ga, 0,
                    (hipStream_t)stream);
   });
 }
@@ -1637,7 +1638,7 @@ int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, i
     REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && dgemm_supported(M, N, K, S, epi), MS_EINVAL,
             "dgemm shape unsupported (M <= 256, N % 64 == 0, K % (64 S) == 0, S > 1 only for fp32 slabs)");
     REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "dgemm row scale: one-tile statistics only");
-    launch_dgemm((const bf16_t*)X, (const bf16_t*)W, out, M, N, K, S, ldo, epi, (hipStream_t)stream, &g_op_rs);
+    launch_dgemm((const f16_t*)X, (const f16_t*)W, out, M, N, K, S, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }
 
@@ -1648,7 +1649,7 @@ int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int3
     REQUIRE(gemv_split_supported(M, N, K, S, op_rs_tiles()), MS_EINVAL,
             "gemv_split shape unsupported (M<=64, (K/S)%64==0, row-scale statistics within kRsStage and LDS)");
     GemvArgs ga;
-    launch_gemv_split((const bf16_t*)X, (const bf16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream,
+    launch_gemv_split((const f16_t*)X, (const f16_t*)W, slabs, M, N, K, S, waves, (hipStream_t)stream,
                       op_gemv_args(ga));
   });
 }
@@ -1661,7 +1662,7 @@ int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* 
     REQUIRE(S == 0 || slabs, MS_EINVAL, "slabs missing");
     REQUIRE(residual_rmsnorm_supported(S, hidden) || (S == 0 && hidden <= 8192), MS_EINVAL,
             "residual_rmsnorm: S <= 8 and hidden <= 3072 (wider rows: S == 0 only)");
-    launch_residual_rmsnorm(x, slabs, S, (const bf16_t*)w, (bf16_t*)y, ssq, rows, hidden,
+    launch_residual_rmsnorm(x, slabs, S, (const f16_t*)w, (f16_t*)y, ssq, rows, hidden,
                             (hipStream_t)stream);
   });
 }
@@ -1674,12 +1675,12 @@ int ms_op_dequant(int32_t type, const void* blocks, int64_t n_blocks, float* out
   });
 }
 
-int ms_op_quant_rows(int32_t type, const void* blocks, int32_t rows, int32_t K, void* bf16_out,
+int ms_op_quant_rows(int32_t type, const void* blocks, int32_t rows, int32_t K, void* f16_out,
                      void* packed_out, void* stream) {
   return op_guard([&] {
-    REQUIRE(blocks && bf16_out && rows >= 1 && K >= 256 && K % 256 == 0, MS_EINVAL, "bad quant_rows arguments");
+    REQUIRE(blocks && f16_out && rows >= 1 && K >= 256 && K % 256 == 0, MS_EINVAL, "bad quant_rows arguments");
     REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
-    launch_quant_rows(type, (const uint8_t*)blocks, rows, K, (bf16_t*)bf16_out, 16, 0,
+    launch_quant_rows(type, (const uint8_t*)blocks, rows, K, (f16_t*)f16_out, 16, 0,
                       (uint8_t*)packed_out, 0, (hipStream_t)stream);
   });
 }
@@ -1700,7 +1701,7 @@ int ms_op_qgemv(const void* X, int32_t type, const void* packed, void* out, int3
     q.type0 = type;
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
     GemvArgs ga;
-    launch_qgemv((const bf16_t*)X, q, out, M, N, K, ldo, epi, op_gemv_args(ga), (hipStream_t)stream);
+    launch_qgemv((const f16_t*)X, q, out, M, N, K, ldo, epi, op_gemv_args(ga), (hipStream_t)stream);
   });
 }
 
@@ -1718,7 +1719,7 @@ int ms_op_qgemv_split(const void* X, int32_t type, const void* packed, float* sl
     q.type0 = type;
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
     GemvArgs ga;
-    launch_qgemv_split((const bf16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream, op_gemv_args(ga));
+    launch_qgemv_split((const f16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream, op_gemv_args(ga));
   });
 }
 
@@ -1727,7 +1728,7 @@ int ms_op_rmsnorm(const void* x, const void* w, void* y, float* ssq, int32_t row
   return op_guard([&] {
     REQUIRE(x && w && y && ssq && rows >= 1 && hidden >= 4 && hidden % 4 == 0 && hidden <= 8192, MS_EINVAL,
             "bad rmsnorm shape");
-    launch_rmsnorm((const float*)x, (const bf16_t*)w, (bf16_t*)y, ssq, rows, hidden, row_idx,
+    launch_rmsnorm((const float*)x, (const f16_t*)w, (f16_t*)y, ssq, rows, hidden, row_idx,
                    (hipStream_t)stream);
   });
 }

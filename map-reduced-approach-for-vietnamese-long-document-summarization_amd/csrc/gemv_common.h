@@ -1,4 +1,4 @@
-// gemv_common.h -- pieces shared by the bf16 and the K-quant decode GEMVs.
+// gemv_common.h -- pieces shared by the fp16 and the K-quant decode GEMVs.
 #pragma once
 #include "kernels.h"
 
@@ -22,7 +22,7 @@ __device__ __forceinline__ void lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// X rows [M][K] bf16 (row stride ldx elements) -> LDS image of M rows x 2K bytes, 16-B
+// X rows [M][K] fp16 (row stride ldx elements) -> LDS image of M rows x 2K bytes, 16-B
 // chunk c of row r stored at chunk c ^ (r & 7) (the rows of an MFMA fragment read land on
 // different bank groups).  Copied by LDS DMA (global_load_lds, 1 KiB per wave instruction)
 // and issued BEFORE the weight stream: vmcnt retires loads in issue order, so X loaded
@@ -36,7 +36,7 @@ __host__ __device__ inline size_t gemv_x_lds_bytes(int M, int K) {
 }
 __device__ __forceinline__ int x_lds(int r, int k, int K) { return r * 2 * K + (((k >> 3) ^ (r & 7)) << 4); }
 
-__device__ __forceinline__ void gemv_dma_x(char* smem, const bf16_t* __restrict__ X, int M, int K, int ldx) {
+__device__ __forceinline__ void gemv_dma_x(char* smem, const f16_t* __restrict__ X, int M, int K, int ldx) {
   const int kch = K >> 3, n = M * kch, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   for (int p = threadIdx.x >> 6; p * 64 < n; p += nw) {
     const int P = min(p * 64 + lane, n - 1);
@@ -56,7 +56,7 @@ enum { kXGlobal = 0, kXLds = 1, kXRegs = 2 };
 // 1024-thread gate/up GEMV its second co-resident block), and folded into rinv[row], which the
 // epilogue reads: wave w owns rows w, w + nw, ..; lane l adds tiles l, l + 64, .. in order,
 // then the wave's xor tree.  At most kRsStage partial sums (host-checked).  HOLD kernels (the
-// K-quant GEMV) take one-tile statistics straight into a register of wave 0 instead; the bf16
+// K-quant GEMV) take one-tile statistics straight into a register of wave 0 instead; the fp16
 // GEMV stages them like any other: holding that register across the weight
 // stream took the 1024-thread gate/up GEMV from 63 to 67 VGPRs and cost its second co-resident
 // block (20.8 -> 22.4 us per launch, profiles/r03/v9_rs_hold_ab.txt).
@@ -108,17 +108,17 @@ __device__ __forceinline__ void rs_finish(const char* smem, size_t rinv_off, con
 
 // the deferred row scale exists only for the epilogues of normalised projections
 template <int EPI> constexpr bool gemv_rs_epi() {
-  return EPI == MS_GEMV_EPI_STORE_BF16 || EPI == MS_GEMV_EPI_SWIGLU || EPI == MS_GEMV_EPI_STORE_F32 ||
+  return EPI == MS_GEMV_EPI_STORE_F16 || EPI == MS_GEMV_EPI_SWIGLU || EPI == MS_GEMV_EPI_STORE_F32 ||
          EPI == MS_GEMV_EPI_ROPE_KV;
 }
 
 constexpr int kXRegsMaxFrags = 4;  // MT x (U or 8*SBW/8) fragment pairs a wave may hold (<= 32 VGPRs)
 // X source per GEMV family, measured same-box on MI355X at B = 8 (profiles/r02/v14_x_regs_ab.txt):
 // the K-quant GEMVs take X into registers (Q4_K_M decode 2.023 -> 1.950 ms/step: the dequant
-// work of each wave starts as soon as its own bytes land, with no block barrier), the bf16
+// work of each wave starts as soon as its own bytes land, with no block barrier), the fp16
 // GEMVs keep the LDS image (registers measured 2.25 -> 2.39 ms/step).  MS_GEMV_X=regs /
 // MS_QGEMV_X (below) flip them (A/B tuning).
-// bf16 X source (MS_GEMV_X): "lds" everywhere (default), "regs" everywhere (where MT x U fits),
+// fp16 X source (MS_GEMV_X): "lds" everywhere (default), "regs" everywhere (where MT x U fits),
 // "f32" registers for the split-K slab GEMVs only, "resid" for the residual-epilogue GEMVs only,
 // "both" for those two families
 enum { kGxLds = 0, kGxRegs = 1, kGxF32 = 2, kGxResid = 3, kGxBoth = 4 };
@@ -185,7 +185,7 @@ __device__ __forceinline__ ResidPre resid_prefetch(int M, int N, int ldo, const 
       gemv_elem(threadIdx.x, 1, n0, row, col, c);
       if (row < M && c < rtv && col < N) {
         p.x = ((const float*)out)[(size_t)row * ldo + col];
-        if (ga.xg_out) p.g = bf2f(ga.gamma[col]);
+        if (ga.xg_out) p.g = h2f(ga.gamma[col]);
       }
     }
   }
@@ -240,7 +240,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
       const float g = sum_e(((m * NT + 0) * 64 + l) * 4 + j) * rv;
       const float u = sum_e(((m * NT + 1) * 64 + l) * 4 + j) * rv;
       const int f = (n0 >> 5) * 16 + (l & 15);
-      ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(g / (1.0f + __expf(-g)) * u);
+      ((f16_t*)out)[(size_t)row * ldo + f] = f2h(g / (1.0f + __expf(-g)) * u);
     }
   } else if constexpr (EPI == MS_GEMV_EPI_ROPE_KV) {
     static_assert(MT == 1 && NT == 1, "rope epilogue works on single 16-row tiles");
@@ -254,22 +254,22 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
       for (int e = tid; e < M * 8; e += nthreads) {
         const int row = e >> 3, c = e & 7, i = 8 * t + c;
         const float rv = rsc(row);
-        const float lo = bf2f(f2bf(sum_e(e_of(row, c)) * rv));      // q/k rounded to bf16, then
-        const float hi = bf2f(f2bf(sum_e(e_of(row, c + 8)) * rv));  // rotated in fp32 (as prefill)
+        const float lo = h2f(f2h(sum_e(e_of(row, c)) * rv));      // q/k rounded to fp16, then
+        const float hi = h2f(f2h(sum_e(e_of(row, c + 8)) * rv));  // rotated in fp32 (as prefill)
         const int pos = ga.tok_pos[row];
         const float cs = ga.cos_tab[(size_t)pos * 64 + i], sn = ga.sin_tab[(size_t)pos * 64 + i];
         const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
         const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
-        bf16_t* dst;
+        f16_t* dst;
         if (is_q) {
-          dst = (bf16_t*)out + (size_t)row * ldo + h * kHeadDim;
+          dst = (f16_t*)out + (size_t)row * ldo + h * kHeadDim;
         } else {
           const int slot = ga.tok_slot[row];
           const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
           dst = ga.kv.k + (((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim;
         }
-        dst[i] = f2bf(ra);
-        dst[64 + i] = f2bf(rb);
+        dst[i] = f2h(ra);
+        dst[64 + i] = f2h(rb);
       }
     } else {  // V head: natural order, straight into the cache
       const int h = (n0 - QD - KD) / kHeadDim, d0 = n0 % kHeadDim;
@@ -278,7 +278,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
         const int pos = ga.tok_pos[row], slot = ga.tok_slot[row];
         const int page = ga.kv.block_table[(size_t)slot * ga.kv.max_pages + pos / kPage];
         ga.kv.v[(((size_t)page * ga.kv.n_kv_heads + h) * kPage + pos % kPage) * kHeadDim + d0 + c] =
-            f2bf(sum_e(e_of(row, c)) * rsc(row));
+            f2h(sum_e(e_of(row, c)) * rsc(row));
       }
     }
   } else if constexpr (EPI == MS_GEMV_EPI_RESID_SSQ) {
@@ -294,7 +294,14 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
         const float xo = (ELEMS <= 256 ? pre.x : *px) + sum_e(e);  // pre: resid_prefetch
         *px = xo;
         q = xo * xo;
-        if (ga.xg_out) ga.xg_out[(size_t)row * ldo + col] = f2bf(xo * (ELEMS <= 256 ? pre.g : bf2f(ga.gamma[col])));
+        // the fp32 product, then its fp16 rounding (the oracle's f16(x * g), rmsnorm_kernel's
+        // v_cvt_pk_f16_f32): left visible, the compiler fused x * g -> fp16 into one
+        // v_fma_mixlo_f16, a single rounding of the exact product that differs at ties
+        if (ga.xg_out) {
+          float xg = xo * (ELEMS <= 256 ? pre.g : h2f(ga.gamma[col]));
+          asm volatile("" : "+v"(xg));
+          ga.xg_out[(size_t)row * ldo + col] = f2h(xg);
+        }
       }
 #pragma unroll
       for (int o = 4; o < 64; o <<= 1) q += __shfl_xor(q, o, 64);
@@ -323,7 +330,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
       if (row >= M || col >= N || (NT == 1 && ga.rt > 0 && (l & 15) >= ga.rt)) continue;
       const float v = sum_e(e);
       const size_t o = (size_t)row * ldo + col;
-      if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(v * rsc(row));
+      if constexpr (EPI == MS_GEMV_EPI_STORE_F16) ((f16_t*)out)[o] = f2h(v * rsc(row));
       else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += v;
       else ((float*)out)[o] = v * rsc(row);
     }

@@ -3,10 +3,10 @@
 // Replaces ggml's attention (mul_mat+soft_max / flash_attn_ext) inside Ollama
 // (SURVEY.md §2 'ggml op replaced', §8a rows A8/A9).  head_dim 128, any GQA group.
 //
-// KV cache: pool[page][kv_head][64 tokens][128] bf16, one page = one 64-key tile;
+// KV cache: pool[page][kv_head][64 tokens][128] fp16, one page = one 64-key tile;
 // a per-sequence block table maps logical tile -> page (engine.cpp owns the pages).
 //
-// Both kernels use the "swapped" orientation on v_mfma_f32_16x16x32_bf16:
+// Both kernels use the "swapped" orientation on v_mfma_f32_16x16x32_f16:
 //   S^T = K . Q^T     (A = K rows from LDS/HBM, B = Q fragments held in VGPRs)
 //   O^T += V^T . P^T  (A = V^T via ds_read_b64_tr_b16 from a row-major V tile,
 //                      B = P^T taken straight from the S^T accumulators)
@@ -28,7 +28,7 @@ __device__ __forceinline__ int k_swz(int row, int ch) { return row * 256 + ((ch 
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * 256 + ((ch ^ ((row & 7) << 1)) << 4); }
 
 // A operand of O^T += V^T P^T for d-tile dt, k-step ks: two transposed 4x16 reads.
-__device__ __forceinline__ bf16x8 load_vt(const char* vs, int dt, int ks, int lane) {
+__device__ __forceinline__ f16x8 load_vt(const char* vs, int dt, int ks, int lane) {
   const int g = lane >> 4, li = lane & 15, q = li >> 2, p = li & 3;
   const int r0 = 32 * ks + 4 * g + q, r1 = r0 + 16;
   const int ch = 2 * dt + (p >> 1), sub = (p & 1) * 8;
@@ -37,57 +37,49 @@ __device__ __forceinline__ bf16x8 load_vt(const char* vs, int dt, int ks, int la
   s4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS_AS s4*)(vs + v_swz(r1, ch) + sub));
   // a vector concatenation (register adjacency): building the 8 shorts element by element
   // compiled to sdwa or/shift repacking, ~80 VALU instructions per attention tile
-  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+  return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
-// B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1.  P enters the
-// P.V MFMAs as TWO bf16 operands, hi = bf16(p) and lo = bf16(p - hi), one MFMA each on the
-// same V^T fragment: p = hi + lo to ~16 bits, so P.V is fp32-accurate.  With hi alone the
-// rounding of P (2^-9 relative) made the attention output differ from the exact-softmax
-// arithmetic by ~1e-3, which the bf16 rounding of the output doubled and 28 layers compounded
-// to ~2e-2 in the final logits (tests/test_gpu_golden28.py; the Ollama CPU path rounds P to
-// fp16, 2^-11).
-__device__ __forceinline__ bf16x8 pack_p(const f32x4& a, const f32x4& b) {
+// B operand P^T for k-step ks from the probabilities of m-tiles 2ks, 2ks+1, rounded to fp16
+// (2^-11 relative): the rounding ggml applies to the softmax output before its F16 V.P matmul
+// (DESIGN.md section 2).  Round 3 fed bf16 P as two halves (hi + lo, two MFMAs per V^T
+// fragment) to keep P.V fp32-accurate; fp16 P needs one.
+__device__ __forceinline__ f16x8 pack_p(const f32x4& a, const f32x4& b) {
   typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  u4 v = {pack2bf(a[0], a[1]), pack2bf(a[2], a[3]), pack2bf(b[0], b[1]), pack2bf(b[2], b[3])};
-  return __builtin_bit_cast(bf16x8, v);
-}
-__device__ __forceinline__ bf16x8 pack_p_lo(const f32x4& a, const f32x4& b, bf16x8 hi) {
-  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-  const u4 h = __builtin_bit_cast(u4, hi);
-  auto lo16 = [](uint32_t w) { return __uint_as_float(w << 16); };
-  auto hi16 = [](uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); };
-  u4 v = {pack2bf(a[0] - lo16(h[0]), a[1] - hi16(h[0])), pack2bf(a[2] - lo16(h[1]), a[3] - hi16(h[1])),
-          pack2bf(b[0] - lo16(h[2]), b[1] - hi16(h[2])), pack2bf(b[2] - lo16(h[3]), b[3] - hi16(h[3]))};
-  return __builtin_bit_cast(bf16x8, v);
+  u4 v = {pack2h(a[0], a[1]), pack2h(a[2], a[3]), pack2h(b[0], b[1]), pack2h(b[2], b[3])};
+  return __builtin_bit_cast(f16x8, v);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // decode KV pages (plain loads: non-temporal ones measured slower, 2.45 vs 2.29 ms per decode
 // step, profiles/r01 v5_nt_stream_ab_rejected)
-__device__ __forceinline__ u32x4 ld_stream(const bf16_t* p) { return *(const u32x4*)p; }
+__device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x4*)p; }
 
 // ============================================================ prefill (varlen, causal)
 // 1-D grid over (q-block, head group), heaviest q-blocks first for every head group; block
-// 256 = 4 waves x 16 query rows, GB q heads of ONE kv head (GQA group, or a divisor of it).
-// Each K fragment read from LDS feeds GB MFMAs (S^T of the GB heads) and each V^T fragment
-// GB MFMAs (O^T of the GB heads): LDS read traffic per MFMA drops GB-fold, and a K/V tile
-// is fetched from HBM once per GB heads instead of once per head.  The online softmax works
-// on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)) with a lazily moved reference
-// max (below); the O rescale is skipped when no query column of the wave moved it; the
-// causal / sequence-end mask is applied only on tiles that can cross it.
-// K/V tiles reach LDS by DMA (global_load_lds, no register staging and no ds_write), two
-// buffers: tile t+1 is in flight while tile t is multiplied, one barrier per tile.  The
-// swizzles are applied on the DMA source (lane i of a 1-KiB piece lands at chunk i % 16 of
-// row i / 16, so it loads the global chunk that belongs there); rows past the sequence
-// load the last valid row instead (finite values under P = 0: never NaN * 0 in P.V).
+// 512 = 8 waves x 16 query rows (kPrefillQRows = 128), GB q heads of ONE kv head (GQA group, or
+// a divisor of it).  Each K fragment read from LDS feeds GB MFMAs (S^T of the GB heads) and each
+// V^T fragment GB MFMAs (O^T of the GB heads), and each K/V tile is fetched once per 128 query
+// rows x GB heads.  Two waves per SIMD (launch bounds 512, 1: <= 256 registers a wave, the O
+// accumulators of the GB heads in AGPRs): one wave's softmax and LDS reads run under the other's
+// MFMAs -- the round-3 kernel (4 waves x 16 rows, hi + lo bf16 P) held 240 VGPRs + 148 AGPRs at
+// one wave per SIMD and could not hide its own QK -> softmax -> PV chain.  The online softmax
+// works on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)) with a lazily moved reference
+// max (below); the O rescale is skipped when no query column of the wave moved it; the causal /
+// sequence-end mask is applied only on tiles that can cross it, and a wave skips the tiles that
+// lie wholly after its last query.  K/V tiles reach LDS by DMA (global_load_lds, no register
+// staging and no ds_write), two buffers: tile t+1 is in flight while tile t is multiplied, one
+// barrier per tile.  The swizzles are applied on the DMA source (lane i of a 1-KiB piece lands
+// at chunk i % 16 of row i / 16, so it loads the global chunk that belongs there); rows past
+// the sequence load the last valid row instead (finite values under P = 0: never NaN * 0 in P.V).
 template <int GB>
-__global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __restrict__ qkv,
-                                                              bf16_t* __restrict__ out, int Hq,
+__global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __restrict__ qkv,
+                                                              f16_t* __restrict__ out, int Hq,
                                                               int Hk, KVView kv, PrefillAttnArgs a,
                                                               float scale_log2) {
-  // [K|V tile buffer 0][K|V tile buffer 1][Q of the GB heads, 16 KB each]
-  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + GB * 16384];
+  constexpr int QR = kPrefillQRows;  // 128 query rows per block
+  // [K|V tile buffer 0][K|V tile buffer 1][Q of the GB heads, QR x 256 B each]: 160 KiB at GB = 3
+  __shared__ __attribute__((aligned(16))) char smem[2 * 32768 + GB * QR * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
   const int ngrp = Hq / GB;
@@ -98,22 +90,23 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
   const int slot = a.seq_slot[sq];
   const int kvh = h0 / (Hq / Hk);
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
-  const int qi = qb * 64 + wave * 16 + r;
+  const int q0 = qb * QR + wave * 16;  // the wave's first query (sequence-relative)
+  const int qi = q0 + r;
   const int qpos = kvlen - qlen + qi;
-  const int wave_qpos0 = kvlen - qlen + qb * 64 + wave * 16;  // the wave's first query
+  const int wave_qpos0 = kvlen - qlen + q0;
+  const int wave_qlast = kvlen - qlen + min(q0 + 15, qlen - 1);  // keys after it: nothing to do
+  const bool wave_live = q0 < qlen;
 
-  // Q fragments live in LDS (each wave reads back only its own 16 rows, swizzled like K):
-  // held in registers they pushed the GB = 3 kernel past 256 VGPRs, and the compiler then
-  // shuttled values through AGPRs (~700 v_accvgpr moves)
+  // Q fragments live in LDS (each wave reads back only its own 16 rows, swizzled like K)
   char* qimg = smem + 2 * 32768;
   const int qrow_l = wave * 16 + r;
   {
-    const bf16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h0 * kHeadDim;
+    const f16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h0 * kHeadDim;
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh)
 #pragma unroll
       for (int s = 0; s < 4; ++s)
-        *(uint4*)(qimg + hh * 16384 + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
+        *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
   }
   f32x4 o[GB][8];
   float m_run[GB], l_run[GB];
@@ -125,12 +118,12 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
     for (int i = 0; i < 8; ++i) o[hh][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const int q_last = min(qb * 64 + 63, qlen - 1);
+  const int q_last = min(qb * QR + QR - 1, qlen - 1);
   const int kv_end = kvlen - qlen + q_last + 1;  // keys visible to the block's last query
   const int ntiles = (kv_end + 63) / 64;
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
 
-  // this wave's 8 DMA pieces of a tile: piece J = 8*wave + i covers rows 4(J % 16) ..+3 of
+  // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
   // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
   auto dma_tile = [&](int t, int buf) {
     const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];
@@ -138,12 +131,12 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
     const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
     char* img = smem + buf * 32768;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int J = 8 * wave + i, isv = J >> 4;
+    for (int i = 0; i < 4; ++i) {
+      const int J = 4 * wave + i, isv = J >> 4;
       const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
       const int srow = min(row, lim - 1);
       const int sch = isv ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
-      const bf16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
+      const f16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (LDS_AS void*)(img + isv * 16384 + 4 * (J & 15) * 256), 16, 0, 0);
     }
@@ -155,6 +148,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + 1 < ntiles) dma_tile(t + 1, (t + 1) & 1);
+    if (!wave_live || t * 64 > wave_qlast) continue;  // wave-uniform: keys after every query
     const char* ks_ = smem + (t & 1) * 32768;
     const char* vs_ = ks_ + 16384;
 
@@ -165,10 +159,10 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       for (int hh = 0; hh < GB; ++hh) sc[hh][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const bf16x8 kf = *(const bf16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
+        const f16x8 kf = *(const f16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh)
-          sc[hh][mt] = mfma16(kf, *(const bf16x8*)(qimg + hh * 16384 + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
+          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
       }
     }
     // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
@@ -185,7 +179,7 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
             for (int hh = 0; hh < GB; ++hh) sc[hh][mt][j] = -INFINITY;
         }
     }
-    bf16x8 pf[GB][2], pl[GB][2];
+    f16x8 pf[GB][2];
     bool rescale = false;
     float alpha[GB];
 #pragma unroll
@@ -198,9 +192,9 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       // lazy rescale: the running max only moves when a tile's max exceeds it by more than
-      // 8 in log2 units (p <= 2^8 is harmless in fp32 and for the bf16 rounding of P), so
-      // after the first tiles the O accumulators (held in AGPRs) are rarely rescaled;
-      // O / l is unchanged by the choice of reference max
+      // 8 in log2 units (p <= 2^8 is harmless in fp32 and in fp16 P), so after the first
+      // tiles the O accumulators are rarely rescaled; O / l is unchanged by the choice of
+      // reference max
       const float m_new = fmaxf(m_run[hh], mx);
       const bool grow = m_new != m_run[hh] && !((m_new - m_run[hh]) * scale_log2 <= 8.f);
       const float m_use = grow ? m_new : m_run[hh];
@@ -222,8 +216,6 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
       m_run[hh] = m_use;
       pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
-      pl[hh][0] = pack_p_lo(sc[hh][0], sc[hh][1], pf[hh][0]);
-      pl[hh][1] = pack_p_lo(sc[hh][2], sc[hh][3], pf[hh][1]);
     }
     if (__ballot(rescale) != 0) {
 #pragma unroll
@@ -235,38 +227,35 @@ __global__ __launch_bounds__(256, 1) void attn_prefill_kernel(const bf16_t* __re
     for (int kstep = 0; kstep < 2; ++kstep)
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
-        const bf16x8 vt = load_vt(vs_, dt, kstep, lane);
+        const f16x8 vt = load_vt(vs_, dt, kstep, lane);
 #pragma unroll
-        for (int hh = 0; hh < GB; ++hh) {
-          o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
-          o[hh][dt] = mfma16(vt, pl[hh][kstep], o[hh][dt]);
-        }
+        for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
       }
   }
-  if (qi < qlen) {
+  if (wave_live && qi < qlen) {
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh) {
       const float inv = 1.0f / l_run[hh];
-      bf16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + (h0 + hh) * kHeadDim;
+      f16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + (h0 + hh) * kHeadDim;
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
         uint2 w;
-        w.x = pack2bf(o[hh][dt][0] * inv, o[hh][dt][1] * inv);
-        w.y = pack2bf(o[hh][dt][2] * inv, o[hh][dt][3] * inv);
+        w.x = pack2h(o[hh][dt][0] * inv, o[hh][dt][1] * inv);
+        w.y = pack2h(o[hh][dt][2] * inv, o[hh][dt][3] * inv);
         *(uint2*)(orow + dt * 16 + 4 * g) = w;
       }
     }
   }
 }
 
-void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s) {
   if (a.n_qblk <= 0) return;
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
   const int G = Hq / Hk;
   const int gb = (G % 3 == 0) ? 3 : (G % 2 == 0) ? 2 : 1;
   const dim3 grid(a.n_qblk * (Hq / gb));
-#define AP(GB_) MS_LAUNCH(attn_prefill_kernel<GB_>, grid, dim3(256), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
+#define AP(GB_) MS_LAUNCH(attn_prefill_kernel<GB_>, grid, dim3(512), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
   if (gb == 3) AP(3);
   else if (gb == 2) AP(2);
   else AP(1);
@@ -278,16 +267,16 @@ void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView 
 // a whole page (K as MFMA fragments + V rows, 32 KB) in flight before its first MFMA.  The G
 // query heads of the kv head are MFMA columns 0..G-1.  Per-wave (m, l, O^T) are merged in LDS
 // (reusing the waves' V images); each block writes one partial (m, l, o[128]) per (b, q head,
-// split), and attn_decode_combine_kernel merges the nsplit partials into the bf16 output.
+// split), and attn_decode_combine_kernel merges the nsplit partials into the fp16 output.
 // With the deferred RMSNorm (kernels.h RowScale) the prologue also folds the row's norm
 // statistics and scales q / k / v by r before rounding them.
 //
 // FROM_SLABS (the fused decode chain): the QKV projection arrives as S fp32 split-K slabs
 // [S][B][(Hq+2Hk)*128] with Q/K rows rope-permuted (k_gemv.hip).  The prologue adds the
-// slabs (slab order), rounds q/k/v to bf16, applies RoPE in fp32 and rounds again -- the
+// slabs (slab order), rounds q/k/v to fp16, applies RoPE in fp32 and rounds again -- the
 // arithmetic of rope_kv_kernel -- and the block that owns the new token's page writes its
 // K/V into the cache (for later steps) and patches them into the page it holds in
-// registers / LDS.  Otherwise q comes from bf16 qkv rows already roped (rope_kv_kernel).
+// registers / LDS.  Otherwise q comes from fp16 qkv rows already roped (rope_kv_kernel).
 constexpr int kSplitPages = 4;  // = waves per block
 constexpr int kMaxGroup = 8;    // q heads per kv head
 constexpr int kMaxSlabs = 8;    // QKV split-K slabs (engine kMaxSplit)
@@ -357,9 +346,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   const int pg0 = split * kSplitPages * ppw + wave;
   const int pend = min((split + 1) * kSplitPages * ppw, (len + kPage - 1) / kPage);
   const int pos = len - 1;               // the new token
-  bf16_t* qn = (bf16_t*)(smem + 4 * 16384);  // [G][128] roped q
-  bf16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
-  bf16_t* vn = kn + kHeadDim;                 // [128] v of the new token
+  f16_t* qn = (f16_t*)(smem + 4 * 16384);  // [G][128] roped q
+  f16_t* kn = qn + kMaxGroup * kHeadDim;     // [128] roped k of the new token
+  f16_t* vn = kn + kHeadDim;                 // [128] v of the new token
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
   constexpr int NWB = kSplitPages;  // waves per block: a wave's pages are NWB apart
 
@@ -408,7 +397,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 
   if constexpr (FROM_SLABS) {
     const bool owns_new = (pos / kPage) / (kSplitPages * ppw) == split;  // block-uniform
-    float* raw = (float*)smem;  // [(G+2)][128] bf16-rounded sums; aliases wave 0's V image
+    float* raw = (float*)smem;  // [(G+2)][128] fp16-rounded sums; aliases wave 0's V image
     const size_t sstride = (size_t)a.B * row_stride;
     const float* src = qa.slabs + (size_t)b * row_stride;
     const float rcs = qa.cos_tab[(size_t)pos * 64 + (tid & 63)];  // this thread's rope pair i
@@ -435,7 +424,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 #pragma unroll
       for (int q = 1; q < kMaxSlabs; ++q)
         if (q < qa.S) acc += sv[i][q];
-      if (e < nvec) raw[e] = bf2f(f2bf(acc * rrow));
+      if (e < nvec) raw[e] = h2f(f2h(acc * rrow));
     }
     __syncthreads();
     const int nrot = (G + (owns_new ? 1 : 0)) * 64;  // (head, i) pairs: the q heads, then k
@@ -445,11 +434,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       const float cs = rcs, sn = rsn;
       const float ra = __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn));
       const float rb = __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
-      bf16_t* dst = hh < G ? qn + hh * kHeadDim : kn;
-      dst[i] = f2bf(ra);
-      dst[64 + i] = f2bf(rb);
+      f16_t* dst = hh < G ? qn + hh * kHeadDim : kn;
+      dst[i] = f2h(ra);
+      dst[64 + i] = f2h(rb);
     }
-    if (owns_new && tid < kHeadDim) vn[tid] = f2bf(raw[(G + 1) * kHeadDim + tid]);
+    if (owns_new && tid < kHeadDim) vn[tid] = f2h(raw[(G + 1) * kHeadDim + tid]);
     __syncthreads();  // raw consumed (wave 0 may stage V); qn/kn/vn ready
     if (owns_new && tid < kHeadDim) {  // the new token's K/V into the cache, for later steps
       const int page = page_id(pos / kPage);
@@ -465,16 +454,16 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
   float m_run = -INFINITY, l_run = 0.f;
 
   if (pg0 < pend) {
-    bf16x8 qf[4];
+    f16x8 qf[4];
     {
       const int hl = min(r, G - 1);
       if constexpr (FROM_SLABS) {
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const bf16x8*)(qn + hl * kHeadDim + 32 * s4 + 8 * g);
+        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const f16x8*)(qn + hl * kHeadDim + 32 * s4 + 8 * g);
       } else {
-        const bf16_t* qrow = qa.qkv + (size_t)b * row_stride + (kvh * G + hl) * kHeadDim;
+        const f16_t* qrow = qa.qkv + (size_t)b * row_stride + (kvh * G + hl) * kHeadDim;
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = as_bf16x8(*(const uint4*)(qrow + 32 * s4 + 8 * g));
+        for (int s4 = 0; s4 < 4; ++s4) qf[s4] = as_f16x8(*(const uint4*)(qrow + 32 * s4 + 8 * g));
       }
     }
     const int off = pos % kPage;
@@ -497,7 +486,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       for (int mt = 0; mt < 4; ++mt) {
         sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(bf16x8, kf[mt][s4]), qf[s4], sc[mt]);
+        for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(f16x8, kf[mt][s4]), qf[s4], sc[mt]);
       }
       const int pid_n = PPWT == 2 ? pid_next : (more ? page_id(pg + kSplitPages) : 0);
       if (more) fetch_k(pid_n);  // K registers are free: next page's K in flight
@@ -543,13 +532,11 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int kstep = 0; kstep < 2; ++kstep) {
-        const bf16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
-        const bf16x8 pl = pack_p_lo(sc[2 * kstep], sc[2 * kstep + 1], pf);
+        const f16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) {
-          const bf16x8 vt = load_vt(vs_, dt, kstep, lane);
+          const f16x8 vt = load_vt(vs_, dt, kstep, lane);
           o[dt] = mfma16(vt, pf, o[dt]);
-          o[dt] = mfma16(vt, pl, o[dt]);
         }
       }
       __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -566,9 +553,9 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       for (int j = 0; j < 4; ++j) mw[r * 130 + 2 + dt * 16 + 4 * g + j] = o[dt][j];
   }
   __syncthreads();
-  for (int idx = tid; idx < G * 130; idx += 256) {
-    const int c = idx / 130, k = idx % 130;
-    float M = -INFINITY;
+  // merged (m, l, O^T) of head c over the block's 4 waves: k = 0 -> m, 1 -> l, 2.. -> O[k - 2]
+  auto merged = [&](int c, int k, float& M) {
+    M = -INFINITY;
 #pragma unroll
     for (int w = 0; w < 4; ++w) M = fmaxf(M, ((const float*)(smem + w * 16384))[c * 130]);
     float acc = 0.f;
@@ -579,18 +566,24 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
       const float f = (m_w == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_w - M);
       acc += (k == 0) ? 0.f : f * mw[c * 130 + k];
     }
-    const int hq = kvh * G + c;
-    float* dst = ws + (((size_t)b * Hq + hq) * nsplit + split) * 132;
-    dst[k] = (k == 0) ? M : acc;
+    return acc;
+  };
+  for (int idx = tid; idx < G * 130; idx += 256) {
+    const int c = idx / 130, k = idx % 130;
+    float M;
+    const float acc = merged(c, k, M);
+    ws[(((size_t)b * Hq + kvh * G + c) * nsplit + split) * 132 + k] = (k == 0) ? M : acc;
   }
 }
 
 // split combine: out[b][hq*128 + d] = sum_s w_s o_s / sum_s w_s l_s, w_s = 2^(m_s - max m) --
-// its own launch (an in-launch ticket combine by the last-arriving split measured no faster:
-// 2.289 vs 2.294 ms per decode step, its release/acquire chain adds ~4 dependent memory round
-// trips to every block)
+// its own launch.  Merging in the attention kernel instead (the last split of each (b, kv head),
+// told by an agent-scope ticket, sc1 partial stores) measured slower twice: 2.289 vs 2.294 ms per
+// decode step with release / acquire fences (round 2), 2.24 vs 2.13 with write-through stores
+// and one ticket per block (round 4, profiles/r04/v3_attn_fused_combine_rejected_ab.txt): every
+// block's lifetime grows by the drain + ticket round trip.
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
-                                                                  bf16_t* __restrict__ out, int Hq,
+                                                                  f16_t* __restrict__ out, int Hq,
                                                                   int nsplit) {
   // one memory round trip: every (m_s, l_s) pair (wave 0, two splits per lane) and, for
   // nsplit <= 16, every O value of this thread are loaded before the barrier (the O loads
@@ -629,10 +622,10 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
     L += fw[s] * lw[s];
     O += fw[s] * po[s * 132];
   }
-  out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2bf(O / L);
+  out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2h(O / L);
 }
 
-void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
+void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv,
                         DecodeAttnArgs a, float* ws, hipStream_t s) {
   if (a.B <= 0) return;
   if (!attn_decode_supported(a.B, Hq, Hk, a.max_len)) return;  // callers check

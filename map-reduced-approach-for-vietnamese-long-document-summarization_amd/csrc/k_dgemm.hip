@@ -12,7 +12,7 @@
 //  * W streams straight to VGPRs, each wave its own 16 rows, DPF K steps in flight
 //    (32 contiguous bytes per lane per step, as in the GEMV), and stays in flight across
 //    the step's LDS-only barrier (an LDS-DMA X image would force a full vmcnt drain there);
-//  * v_mfma_f32_16x16x32_bf16, the wave's 16 weight rows as MFMA columns, MT m-tiles;
+//  * v_mfma_f32_16x16x32_f16, the wave's 16 weight rows as MFMA columns, MT m-tiles;
 //  * split-K over gridDim.y for the narrow projections (fp32 slabs, folded by the next
 //    residual_rmsnorm / attention prologue exactly like the GEMV's).
 // A row's sum order depends only on (K, split), never on M or on the other rows.
@@ -27,8 +27,8 @@ constexpr int DBN = 64, DBK = 64;
 template <int MT> constexpr int dgemm_dpf() { return MT >= 16 ? 6 : 3; }
 
 template <int MT, int EPI>
-__global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16_t* __restrict__ X,
-                                                      const bf16_t* __restrict__ W,
+__global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const f16_t* __restrict__ X,
+                                                      const f16_t* __restrict__ W,
                                                       void* __restrict__ out, int M, int N, int K,
                                                       int ldk, int ldo, RowScale rs) {
   constexpr int DPF = dgemm_dpf<MT>();
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16
   };
   // W: lane (fr, fg) holds k0 + 16 fg .. +15 of row n0 + 16 wave + fr (32 contiguous bytes),
   // a DPF-slot register ring, DPF K steps in flight; X: the same permuted k order from LDS
-  const bf16_t* wrow = W + (size_t)min(n0 + 16 * wave + fr, N - 1) * ldk + kb + 16 * fg;
+  const f16_t* wrow = W + (size_t)min(n0 + 16 * wave + fr, N - 1) * ldk + kb + 16 * fg;
   uint4 wr[DPF][2];
   load_x(0);
   store_x(0);
@@ -95,10 +95,10 @@ __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         const int row = m * 16 + fr;
-        const bf16x8 x0 = *(const bf16x8*)(xs + row * 128 + (((2 * fg) ^ (row & 7)) << 4));
-        const bf16x8 x1 = *(const bf16x8*)(xs + row * 128 + (((2 * fg + 1) ^ (row & 7)) << 4));
-        acc[m] = mfma16(x0, as_bf16x8(wr[i][0]), acc[m]);
-        acc[m] = mfma16(x1, as_bf16x8(wr[i][1]), acc[m]);
+        const f16x8 x0 = *(const f16x8*)(xs + row * 128 + (((2 * fg) ^ (row & 7)) << 4));
+        const f16x8 x1 = *(const f16x8*)(xs + row * 128 + (((2 * fg + 1) ^ (row & 7)) << 4));
+        acc[m] = mfma16(x0, as_f16x8(wr[i][0]), acc[m]);
+        acc[m] = mfma16(x1, as_f16x8(wr[i][1]), acc[m]);
       }
       // (b) X(t+1) into the other stage (every wave finished reading it before the last sync)
       store_x(buf ^ 1);
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16
         const int row = m * 16 + 4 * fg + j;
         if (row < M && f < N / 2) {
           const float gte = acc[m][j];
-          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(gte / (1.0f + __expf(-gte)) * u[j]);
+          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(gte / (1.0f + __expf(-gte)) * u[j]);
         }
       }
     }
@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256, MT >= 16 ? 1 : 2) void dgemm_kernel(const bf16
         const int row = m * 16 + 4 * fg + j;
         if (row >= M) continue;
         const size_t o = (size_t)row * ldo + col;
-        if constexpr (EPI == MS_GEMV_EPI_STORE_BF16) ((bf16_t*)out)[o] = f2bf(acc[m][j]);
+        if constexpr (EPI == MS_GEMV_EPI_STORE_F16) ((f16_t*)out)[o] = f2h(acc[m][j]);
         else if constexpr (EPI == MS_GEMV_EPI_ADD_F32) ((float*)out)[o] += acc[m][j];
         else ((float*)out)[o] = acc[m][j];
       }
@@ -178,13 +178,13 @@ bool dgemm_supported(int M, int N, int K, int S, int epi) {
 }
 
 template <int MT>
-static void dgemm_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo,
+static void dgemm_go(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo,
                      int epi, const RowScale& rs, hipStream_t s) {
   const dim3 grid(N / DBN, S), blk(256);
   const int Ks = K / S;
   switch (epi) {
 #define DG(E_) MS_LAUNCH((dgemm_kernel<MT, E_>), grid, blk, 0, s, X, W, out, M, N, Ks, K, ldo, rs)
-    case MS_GEMV_EPI_STORE_BF16: DG(MS_GEMV_EPI_STORE_BF16); break;
+    case MS_GEMV_EPI_STORE_F16: DG(MS_GEMV_EPI_STORE_F16); break;
     case MS_GEMV_EPI_ADD_F32: DG(MS_GEMV_EPI_ADD_F32); break;
     case MS_GEMV_EPI_SWIGLU: DG(MS_GEMV_EPI_SWIGLU); break;
     case MS_GEMV_EPI_ARGMAX: DG(MS_GEMV_EPI_ARGMAX); break;
@@ -194,7 +194,7 @@ static void dgemm_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, 
 }
 
 // rs: the deferred RMSNorm scale of the output rows, one-tile partials only (or null)
-void launch_dgemm(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+void launch_dgemm(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
                   hipStream_t s, const RowScale* rs_in) {
   if (!dgemm_supported(M, N, K, S, epi)) return;  // callers check
   RowScale rs{};

@@ -2,12 +2,12 @@
 //
 // Replaces ggml mul_mat for QKV / O / gate+up / down over the packed prompt tokens
 // of every chunk in flight (SURVEY.md §2 "ggml op replaced", §8a row A8).
-// out (epilogue) A[M][K] . W[N][K]^T ; A = activations (bf16, K-contiguous),
-// W = nn.Linear weight [out][in] (bf16, K-contiguous): an "NT" GEMM, so both MFMA
+// out (epilogue) A[M][K] . W[N][K]^T ; A = activations (fp16, K-contiguous),
+// W = nn.Linear weight [out][in] (fp16, K-contiguous): an "NT" GEMM, so both MFMA
 // operands are read along K and no transpose is ever needed.
 //
 // Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4 tiles of
-// v_mfma_f32_16x16x32_bf16.  Both operands stream HBM->LDS with global_load_lds
+// v_mfma_f32_16x16x32_f16.  Both operands stream HBM->LDS with global_load_lds
 // dwordx4 (1 KiB per wave-instruction, lane-linear); the LDS image is XOR-swizzled
 // by pre-swizzling the per-lane SOURCE address (chunk ^ (row & 7)), so the
 // ds_read_b128 fragment reads are conflict-free (cdna_hip_programming.md §5.4 rule 21,
@@ -32,8 +32,8 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 __device__ __forceinline__ float silu_mul(float g, float u) { return g / (1.0f + __expf(-g)) * u; }
 
 template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__ A,
-                                                     const bf16_t* __restrict__ W,
+__global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ A,
+                                                     const f16_t* __restrict__ W,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, RowScale rs) {
   // 64 KiB of tiles + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
@@ -52,8 +52,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
   const int m0 = tm * GBM, n0 = tn * GBN;
 
   // per-lane DMA sources: wave-instruction i = wave*4+t covers tile rows 8i..8i+7
-  const bf16_t* a_src[4];
-  const bf16_t* b_src[4];
+  const f16_t* a_src[4];
+  const f16_t* b_src[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     const int r = (wave * 4 + t) * 8 + (lane >> 3);
@@ -95,18 +95,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
     const char* Bs = As + 16384;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      bf16x8 af[4], bfr[4];
+      f16x8 af[4], bfr[4];
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const int row = wm * 64 + m * 16 + fr;
         const int ch = (4 * s + fg) ^ (row & 7);
-        af[m] = *(const bf16x8*)(As + row * 128 + ch * 16);
+        af[m] = *(const f16x8*)(As + row * 128 + ch * 16);
       }
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const int row = wn * 64 + n * 16 + fr;
         const int ch = (4 * s + fg) ^ (row & 7);
-        bfr[n] = *(const bf16x8*)(Bs + row * 128 + ch * 16);
+        bfr[n] = *(const f16x8*)(Bs + row * 128 + ch * 16);
       }
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
           const int col = n0 + wn * 64 + n * 16;  // multiple of 32
           if (col >= N) continue;
           const int f = (col >> 5) * 16 + fr;
-          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[m][n][j] * rv, acc[m][n + 1][j] * rv));
+          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[m][n][j] * rv, acc[m][n + 1][j] * rv));
         }
       } else {
 #pragma unroll
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16_t* __restrict__
           const int col = n0 + wn * 64 + n * 16 + fr;
           if (col >= N) continue;
           const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[m][n][j] * rv);
+          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[m][n][j] * rv);
           else if constexpr (EPI == 1) ((float*)out)[o] += acc[m][n][j];
           else ((float*)out)[o] = acc[m][n][j] * rv;
         }
@@ -215,8 +215,8 @@ constexpr int TBM = 256, TBN = 256, TBK = 64;
 __device__ __forceinline__ int swz2(int r) { return (r >> 1) & 7; }
 
 template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restrict__ A,
-                                                        const bf16_t* __restrict__ W,
+__global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict__ A,
+                                                        const f16_t* __restrict__ W,
                                                         void* __restrict__ out, int M, int N, int K,
                                                         int ldo, RowScale rs) {
   // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
       dst_row[u][i] = tr - (lane >> 3);  // first row of the instruction's 8-row group
     }
   auto stage = [&](int buf, int u, int k0) {
-    const bf16_t* base = u < 2 ? A : W;
+    const f16_t* base = u < 2 ? A : W;
     char* img = smem + buf * 65536 + (u < 2 ? 0 : 32768);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 af[4][2], bfr[2][2];
+  f16x8 af[4][2], bfr[2][2];
 
   auto read_a = [&](int buf, int qa) {
     const char* img = smem + buf * 65536;
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int row = wr * 128 + qa * 64 + m * 16 + fr;
-        af[m][s2] = *(const bf16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
+        af[m][s2] = *(const f16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
       }
   };
   auto read_b = [&](int buf, int qb) {
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int row = wc * 64 + qb * 32 + n * 16 + fr;
-        bfr[n][s2] = *(const bf16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
+        bfr[n][s2] = *(const f16x8*)(img + row * 128 + (((4 * s2 + fg) ^ sw) << 4));
       }
   };
   auto mma = [&](int qa, int qb) {
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
           const int col = n0 + wc * 64 + ni * 16;  // multiple of 32
           if (col >= N) continue;
           const int f = (col >> 5) * 16 + fr;
-          ((bf16_t*)out)[(size_t)row * ldo + f] = f2bf(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
+          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
         }
       } else {
 #pragma unroll
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const bf16_t* __restric
           const int col = n0 + wc * 64 + ni * 16 + fr;
           if (col >= N) continue;
           const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((bf16_t*)out)[o] = f2bf(acc[mi][ni][j] * rv);
+          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[mi][ni][j] * rv);
           else if constexpr (EPI == 1) ((float*)out)[o] += acc[mi][ni][j];
           else ((float*)out)[o] = acc[mi][ni][j] * rv;
         }
@@ -438,7 +438,7 @@ static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning 
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
-void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,
+void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  hipStream_t s, const RowScale* rs_in) {
   if (M <= 0) return;
   RowScale rs{};

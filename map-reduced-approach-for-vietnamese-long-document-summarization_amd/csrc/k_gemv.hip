@@ -2,7 +2,7 @@
 //
 // Replaces ggml mul_mat at decode time: every decode step
 // multiplies the B <= 64 in-flight sequences' rows by every weight matrix once, so the
-// step is HBM-bound on the 6.4 GB of bf16 weights.  Design for that:
+// step is HBM-bound on the 6.4 GB of fp16 weights.  Design for that:
 //  * one block per 16*NT weight rows, the whole K range split over the block's waves
 //    (reduced through LDS) -- no cross-block split-K, so no fences or tickets;
 //  * every wave issues the loads of its whole K slice (U steps of 64) before its
@@ -10,11 +10,11 @@
 //    §5 'GEMV / M <= 16'), 32 contiguous bytes per lane per step, so a wave-instruction
 //    pair covers 16 full 128-B lines; X (tiny, L2-resident) is staged once per block
 //    into LDS (row stride 2K+16 B: conflict-free fragment reads) while W is in flight;
-//  * v_mfma_f32_16x16x32_bf16 with the sequences as MFMA rows (M padded to 16*MT);
+//  * v_mfma_f32_16x16x32_f16 with the sequences as MFMA rows (M padded to 16*MT);
 //    both operands use the same permuted k order (lane group g holds k0+16g..+15),
 //    which leaves every dot product unchanged.
 // Fusions that remove whole launches from the decode step:
-//  * the deferred RMSNorm (kernels.h RowScale): X is already bf16(x * g), written by the
+//  * the deferred RMSNorm (kernels.h RowScale): X is already f16(x * g), written by the
 //    producer of x (RESID_SSQ epilogue or a norm kernel) with per-tile sums of x^2; the block
 //    loads its rows' partial sums ahead of everything else and scales its output rows by
 //    rinv in the epilogue -- no norm launch between the residual update and the projection
@@ -23,7 +23,7 @@
 //  * EPI_ROPE_KV (QKV): Q/K rows are uploaded rope-permuted (dims i and i+64 in one
 //    16-row tile), so the epilogue applies RoPE, writes Q for attention and scatters
 //    K/V into the paged cache;
-//  * bf16 store, fp32 residual add (O, down), SwiGLU on 16-row-interleaved gate/up,
+//  * fp16 store, fp32 residual add (O, down), SwiGLU on 16-row-interleaved gate/up,
 //    fp32 store (lm_head logits).
 // Results are deterministic and independent of the batch composition: a row's sum
 // order depends only on (N, K), never on M or on the other rows.
@@ -83,8 +83,8 @@ static size_t gemv_lds_bytes(const GemvPlan& p, int M, int K, bool xlds, const R
 // rinv_off: LDS byte offset of the deferred-norm factors (gemv_rinv_offset).  (Two
 // 1024-thread gate/up blocks share a CU at <= 64 VGPRs: 58 / 60 without / with the row scale.)
 template <int MT, int NT, int EPI, int U, int XM, bool RS>
-__global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X,
-                                                    const bf16_t* __restrict__ W,
+__global__ __launch_bounds__(1024) void gemv_kernel(const f16_t* __restrict__ X,
+                                                    const f16_t* __restrict__ W,
                                                     void* __restrict__ out, int M, int N, int K,
                                                     int ldk, int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -113,7 +113,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
-        const bf16_t* xg = X + (size_t)min(m * 16 + fr, M - 1) * ldk + kbeg + u * 64 + 16 * fg;
+        const f16_t* xg = X + (size_t)min(m * 16 + fr, M - 1) * ldk + kbeg + u * 64 + 16 * fg;
         xr[u][m][0] = ldg16(xg);
         xr[u][m][1] = ldg16(xg + 8);
       }
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int wrow = NT == 1 ? n0 + min(fr, rt - 1) : n0 + n * 16 + fr;
-    const bf16_t* wp = W + (size_t)min(wrow, N - 1) * ldk + kbeg + 16 * fg;
+    const f16_t* wp = W + (size_t)min(wrow, N - 1) * ldk + kbeg + 16 * fg;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       w[u][n][0] = ldw16(wp + u * 64);
@@ -150,23 +150,23 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       const int xrow = min(m * 16 + fr, M - 1);
-      bf16x8 x0, x1;
+      f16x8 x0, x1;
       if constexpr (XM == kXRegs) {
-        x0 = as_bf16x8(xr[u][m][0]);
-        x1 = as_bf16x8(xr[u][m][1]);
+        x0 = as_f16x8(xr[u][m][0]);
+        x1 = as_f16x8(xr[u][m][1]);
       } else if constexpr (XM == kXLds) {
         const int k0 = kbeg + u * 64 + 16 * fg;
-        x0 = *(const bf16x8*)(smem + x_lds(xrow, k0, K));
-        x1 = *(const bf16x8*)(smem + x_lds(xrow, k0 + 8, K));
+        x0 = *(const f16x8*)(smem + x_lds(xrow, k0, K));
+        x1 = *(const f16x8*)(smem + x_lds(xrow, k0 + 8, K));
       } else {
-        const bf16_t* xg = X + (size_t)xrow * ldk + kbeg + u * 64 + 16 * fg;
-        x0 = as_bf16x8(ldg16(xg));
-        x1 = as_bf16x8(ldg16(xg + 8));
+        const f16_t* xg = X + (size_t)xrow * ldk + kbeg + u * 64 + 16 * fg;
+        x0 = as_f16x8(ldg16(xg));
+        x1 = as_f16x8(ldg16(xg + 8));
       }
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        acc[m][n] = mfma16(x0, as_bf16x8(w[u][n][0]), acc[m][n]);
-        acc[m][n] = mfma16(x1, as_bf16x8(w[u][n][1]), acc[m][n]);
+        acc[m][n] = mfma16(x0, as_f16x8(w[u][n][0]), acc[m][n]);
+        acc[m][n] = mfma16(x1, as_f16x8(w[u][n][1]), acc[m][n]);
       }
     }
   }
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const bf16_t* __restrict__ X
 }
 
 template <int MT, int NT, int EPI, int U, bool RS>
-static void gemv_go_rs(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+static void gemv_go_rs(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                        const dim3& grid, const dim3& blk, size_t lds, int ro, int ldo, int xm,
                        const GemvArgs& ga, hipStream_t s) {
   if constexpr (MT * U <= kXRegsMaxFrags) {
@@ -193,7 +193,7 @@ static void gemv_go_rs(const bf16_t* X, const bf16_t* W, void* out, int M, int N
 }
 
 template <int MT, int NT, int EPI, int U>
-static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+static void gemv_go(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                     int S, int ldo, const GemvPlan& p, size_t lds, int xm, const GemvArgs& ga,
                     hipStream_t s) {
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
@@ -209,7 +209,7 @@ static void gemv_go(const bf16_t* X, const bf16_t* W, void* out, int M, int N, i
 }
 
 template <int MT, int NT, int EPI>
-static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+static void gemv_go_u(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                       int S, int ldo, const GemvPlan& p, size_t lds, int xm, const GemvArgs& ga,
                       hipStream_t s) {
 #define GU(U_) gemv_go<MT, NT, EPI, U_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xm, ga, s)
@@ -227,12 +227,12 @@ static void gemv_go_u(const bf16_t* X, const bf16_t* W, void* out, int M, int N,
 }
 
 template <int MT>
-static void gemv_go_mt(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+static void gemv_go_mt(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                        int S, int ldo, int epi, const GemvPlan& p, size_t lds, int xm,
                        const GemvArgs& ga, hipStream_t s) {
 #define GE(NT_, E_) gemv_go_u<MT, NT_, E_>(X, W, out, M, N, K, ldk, S, ldo, p, lds, xm, ga, s)
   switch (epi) {
-    case MS_GEMV_EPI_STORE_BF16: GE(1, MS_GEMV_EPI_STORE_BF16); break;
+    case MS_GEMV_EPI_STORE_F16: GE(1, MS_GEMV_EPI_STORE_F16); break;
     case MS_GEMV_EPI_ADD_F32: GE(1, MS_GEMV_EPI_ADD_F32); break;
     case MS_GEMV_EPI_SWIGLU: GE(2, MS_GEMV_EPI_SWIGLU); break;
     case MS_GEMV_EPI_ROPE_KV: GE(1, MS_GEMV_EPI_ROPE_KV); break;
@@ -261,7 +261,7 @@ bool gemv_supported(int M, int N, int K, int epi, int rs_tiles) {
   return gemv_lds_bytes(p, M, K, false, rs) <= kMaxLds;
 }
 
-static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+static void gemv_dispatch(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                           int S, int ldo, int epi, const GemvArgs* ga_in, int force_waves,
                           hipStream_t s) {
   if (M <= 0) return;
@@ -286,13 +286,13 @@ static void gemv_dispatch(const bf16_t* X, const bf16_t* W, void* out, int M, in
   }
 }
 
-void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+void launch_gemv_ex(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, const GemvArgs* ga_in, int force_waves, hipStream_t s) {
   gemv_dispatch(X, W, out, M, N, K, K, 1, ldo, epi, ga_in, force_waves, s);
 }
 
 // tuning hook: W rows of stride ldk >= K elements (padded layouts: HBM channel spread)
-void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+void launch_gemv_strided(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                          int ldo, int epi, hipStream_t s) {
   gemv_dispatch(X, W, out, M, N, K, ldk, 1, ldo, epi, nullptr, 0, s);
 }
@@ -304,7 +304,7 @@ bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles) {
   return gemv_supported(M, N, K / S, MS_GEMV_EPI_STORE_F32, rs_tiles);
 }
 
-void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
+void launch_gemv_split(const f16_t* X, const f16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga) {
   gemv_dispatch(X, W, slabs, M, N, K / S, K, S, N, MS_GEMV_EPI_STORE_F32, ga, force_waves, s);
 }
@@ -344,7 +344,7 @@ void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* 
   MS_LAUNCH(argmax_partials_kernel, dim3(rows), dim3(1024), 0, s, (const float2*)partials, tiles, out);
 }
 
-void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo, int epi,
+void launch_gemv(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  void*, hipStream_t s) {
   launch_gemv_ex(X, W, out, M, N, K, ldo, epi, nullptr, 0, s);
 }

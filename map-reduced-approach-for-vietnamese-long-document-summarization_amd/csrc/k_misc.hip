@@ -12,35 +12,35 @@ thread_local ProfEvents* g_prof = nullptr;
 
 // ---------------------------------------------------------------- embedding
 // x[t][:] = float(E[ids[t]][:]) ; 16-B loads, 32-B stores.  With gamma (a decode step's first
-// layer): also xg[t] = bf16(x[t] * gamma) and ssq[t] = sum of x[t]^2 (a fixed order)
+// layer): also xg[t] = f16(x[t] * gamma) and ssq[t] = sum of x[t]^2 (a fixed order)
 // -- the first QKV projection's input and deferred-norm statistics, with no norm launch.
 __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ ids,
-                                                    const bf16_t* __restrict__ emb, int H,
-                                                    float* __restrict__ x, const bf16_t* __restrict__ gamma,
-                                                    bf16_t* __restrict__ xg, float* __restrict__ ssq) {
+                                                    const f16_t* __restrict__ emb, int H,
+                                                    float* __restrict__ x, const f16_t* __restrict__ gamma,
+                                                    f16_t* __restrict__ xg, float* __restrict__ ssq) {
   __shared__ float red[4];
   const int t = blockIdx.x;
-  const bf16_t* row = emb + (size_t)ids[t] * H;
+  const f16_t* row = emb + (size_t)ids[t] * H;
   float* xo = x + (size_t)t * H;
   float ss = 0.f;
   for (int c = threadIdx.x; c < H / 8; c += blockDim.x) {
     uint4 v = *(const uint4*)(row + c * 8);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     float4 a, b;
-    a.x = __uint_as_float(w[0] << 16); a.y = __uint_as_float(w[0] & 0xFFFF0000u);
-    a.z = __uint_as_float(w[1] << 16); a.w = __uint_as_float(w[1] & 0xFFFF0000u);
-    b.x = __uint_as_float(w[2] << 16); b.y = __uint_as_float(w[2] & 0xFFFF0000u);
-    b.z = __uint_as_float(w[3] << 16); b.w = __uint_as_float(w[3] & 0xFFFF0000u);
+    a.x = h_lo(w[0]); a.y = h_hi(w[0]);
+    a.z = h_lo(w[1]); a.w = h_hi(w[1]);
+    b.x = h_lo(w[2]); b.y = h_hi(w[2]);
+    b.z = h_lo(w[3]); b.w = h_hi(w[3]);
     *(float4*)(xo + c * 8) = a;
     *(float4*)(xo + c * 8 + 4) = b;
     if (gamma) {  // block-uniform
       const uint4 gv = *(const uint4*)(gamma + c * 8);
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
       uint4 o;
-      o.x = pack2bf(a.x * __uint_as_float(gw[0] << 16), a.y * __uint_as_float(gw[0] & 0xFFFF0000u));
-      o.y = pack2bf(a.z * __uint_as_float(gw[1] << 16), a.w * __uint_as_float(gw[1] & 0xFFFF0000u));
-      o.z = pack2bf(b.x * __uint_as_float(gw[2] << 16), b.y * __uint_as_float(gw[2] & 0xFFFF0000u));
-      o.w = pack2bf(b.z * __uint_as_float(gw[3] << 16), b.w * __uint_as_float(gw[3] & 0xFFFF0000u));
+      o.x = pack2h(a.x * h_lo(gw[0]), a.y * h_hi(gw[0]));
+      o.y = pack2h(a.z * h_lo(gw[1]), a.w * h_hi(gw[1]));
+      o.z = pack2h(b.x * h_lo(gw[2]), b.y * h_hi(gw[2]));
+      o.w = pack2h(b.z * h_lo(gw[3]), b.w * h_hi(gw[3]));
       *(uint4*)(xg + (size_t)t * H + c * 8) = o;
       ss += (a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w);
     }
@@ -80,20 +80,20 @@ void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring,
   MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
 }
 
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
-                  const bf16_t* gamma, bf16_t* xg, float* ssq) {
+void launch_embed(const int32_t* ids, int T, const f16_t* emb, int H, float* x, hipStream_t s,
+                  const f16_t* gamma, f16_t* xg, float* ssq) {
   if (T <= 0) return;
   MS_LAUNCH(embed_kernel, dim3(T), dim3(256), 0, s, ids, emb, H, x, gamma, xg, ssq);
 }
 
 // ---------------------------------------------------------------- RMSNorm
 // The GEMM input of a normalised projection (deferred RMSNorm, kernels.h RowScale):
-// y = bf16(x * w) and ssq[r] = sum of x^2 (per thread, the wave tree, then the 4 waves in
+// y = f16(x * w) and ssq[r] = sum of x^2 (per thread, the wave tree, then the 4 waves in
 // order), one 256-thread block per row; the row is read once (<= 8 float4 per thread kept in
 // registers, H <= 8192).  The projection scales its output rows by rs_rinv(ssq[r]).
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ x,
-                                                      const bf16_t* __restrict__ w,
-                                                      bf16_t* __restrict__ y, float* __restrict__ ssq,
+                                                      const f16_t* __restrict__ w,
+                                                      f16_t* __restrict__ y, float* __restrict__ ssq,
                                                       int H, const int32_t* __restrict__ row_idx) {
   __shared__ float red[4];
   const int r = blockIdx.x;
@@ -108,17 +108,17 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
     v[k] = *(const float4*)(xr + c * 4);
     if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
   }
-  bf16_t* yr = y + (size_t)r * H;
+  f16_t* yr = y + (size_t)r * H;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const int c = threadIdx.x + k * 256;
     if (c >= n4) break;
     uint2 wv = *(const uint2*)(w + c * 4);
-    float g0 = __uint_as_float(wv.x << 16), g1 = __uint_as_float(wv.x & 0xFFFF0000u);
-    float g2 = __uint_as_float(wv.y << 16), g3 = __uint_as_float(wv.y & 0xFFFF0000u);
+    float g0 = h_lo(wv.x), g1 = h_hi(wv.x);
+    float g2 = h_lo(wv.y), g3 = h_hi(wv.y);
     uint2 o;
-    o.x = pack2bf(v[k].x * g0, v[k].y * g1);
-    o.y = pack2bf(v[k].z * g2, v[k].w * g3);
+    o.x = pack2h(v[k].x * g0, v[k].y * g1);
+    o.y = pack2h(v[k].z * g2, v[k].w * g3);
     *(uint2*)(yr + c * 4) = o;
   }
   ss = wave_sum(ss);
@@ -127,14 +127,14 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) ssq[r] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, float* ssq, int rows, int H,
+void launch_rmsnorm(const float* x, const f16_t* w, f16_t* y, float* ssq, int rows, int H,
                     const int32_t* row_idx, hipStream_t s) {
   if (rows <= 0) return;
   MS_LAUNCH(rmsnorm_kernel, dim3(rows), dim3(256), 0, s, x, w, y, ssq, H, row_idx);
 }
 
 // Decode: the residual update of a split-K projection fused with the next norm's input.
-// x[r] += (slab_0[r] + slab_1[r] + ... + slab_{S-1}[r]), then y[r] = bf16(x[r] * w) and
+// x[r] += (slab_0[r] + slab_1[r] + ... + slab_{S-1}[r]), then y[r] = f16(x[r] * w) and
 // ssq[r] = sum of x[r]^2 (rmsnorm_kernel's order): the next projection's deferred RowScale.
 // The summation order is fixed (slab order), so the result does not depend on timing or on
 // the other rows.  One block per row; every load (x, w, all S slabs) is issued before the
@@ -143,8 +143,8 @@ template <int S>
 __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict__ x,
                                                                const float* __restrict__ slabs,
                                                                int rows,
-                                                               const bf16_t* __restrict__ w,
-                                                               bf16_t* __restrict__ y,
+                                                               const f16_t* __restrict__ w,
+                                                               f16_t* __restrict__ y,
                                                                float* __restrict__ ssq, int H) {
   constexpr int KMAX = 3;  // float4 per thread: H <= 3072
   __shared__ float red[4];
@@ -189,17 +189,17 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
 #pragma unroll
   for (int k = 0; k < KMAX; ++k)
     if (threadIdx.x + k * 256 < n4) ss += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
-  bf16_t* yr = y + (size_t)r * H;
+  f16_t* yr = y + (size_t)r * H;
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) {
     const int c = threadIdx.x + k * 256;
     if (c >= n4) break;
     if constexpr (S > 0) *(f32x4*)(xr + c * 4) = v[k];
-    const float g0 = __uint_as_float(wv[k].x << 16), g1 = __uint_as_float(wv[k].x & 0xFFFF0000u);
-    const float g2 = __uint_as_float(wv[k].y << 16), g3 = __uint_as_float(wv[k].y & 0xFFFF0000u);
+    const float g0 = h_lo(wv[k].x), g1 = h_hi(wv[k].x);
+    const float g2 = h_lo(wv[k].y), g3 = h_hi(wv[k].y);
     uint2 o;
-    o.x = pack2bf(v[k].x * g0, v[k].y * g1);
-    o.y = pack2bf(v[k].z * g2, v[k].w * g3);
+    o.x = pack2h(v[k].x * g0, v[k].y * g1);
+    o.y = pack2h(v[k].z * g2, v[k].w * g3);
     *(uint2*)(yr + c * 4) = o;
   }
   ss = wave_sum(ss);
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
 
 bool residual_rmsnorm_supported(int S, int H) { return S >= 0 && S <= 8 && H % 4 == 0 && H <= 3072; }
 
-void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
+void launch_residual_rmsnorm(float* x, const float* slabs, int S, const f16_t* w, f16_t* y,
                              float* ssq, int rows, int H, hipStream_t s) {
   if (rows <= 0) return;
   if (H > 3072) {  // wider models: the plain kernel (S = 0 only)
@@ -230,20 +230,20 @@ void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* 
 // weight rows are uploaded in rope_perm order so a 16-row GEMV tile holds dims i and i+64).
 // rotate-half pairs (i, i+64).  One block per token; the token's Q|K part is staged in LDS
 // first because Q is rewritten in place in natural dim order.
-__global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, int Hq, int Hk,
+__global__ __launch_bounds__(256) void rope_kv_kernel(f16_t* __restrict__ qkv, int Hq, int Hk,
                                                       const int32_t* __restrict__ tok_pos,
                                                       const int32_t* __restrict__ tok_slot,
                                                       const float* __restrict__ cos_tab,
                                                       const float* __restrict__ sin_tab,
                                                       KVView kv) {
-  __shared__ __attribute__((aligned(16))) bf16_t st[64 * kHeadDim];  // <= 64 Q+K heads
+  __shared__ __attribute__((aligned(16))) f16_t st[64 * kHeadDim];  // <= 64 Q+K heads
   const int t = blockIdx.x;
   const int pos = tok_pos[t];
   const int slot = tok_slot[t];
   const int page = kv.block_table[(size_t)slot * kv.max_pages + pos / kPage];
   const int off = pos % kPage;
   const int row_elems = (Hq + 2 * Hk) * kHeadDim;
-  bf16_t* row = qkv + (size_t)t * row_elems;
+  f16_t* row = qkv + (size_t)t * row_elems;
   const int qk_elems = (Hq + Hk) * kHeadDim;
   for (int c = threadIdx.x; c < qk_elems / 8; c += blockDim.x)
     *(uint4*)(st + c * 8) = *(const uint4*)(row + c * 8);
@@ -254,15 +254,15 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
     const int i0 = (it & 15) * 4;  // dims i0..i0+3 and 64+i0..64+i0+3
     uint2 olo, ohi;
     if (head < Hq + Hk) {  // Q or K: rotate (from the permuted staging copy)
-      const bf16_t* hp = st + head * kHeadDim;
+      const f16_t* hp = st + head * kHeadDim;
       const uint2 lo = *(const uint2*)(hp + rope_perm(i0));
       const uint2 hi = *(const uint2*)(hp + rope_perm(64 + i0));
       const float4 c = *(const float4*)(cos_tab + (size_t)pos * 64 + i0);
       const float4 sn = *(const float4*)(sin_tab + (size_t)pos * 64 + i0);
-      float a[4] = {__uint_as_float(lo.x << 16), __uint_as_float(lo.x & 0xFFFF0000u),
-                    __uint_as_float(lo.y << 16), __uint_as_float(lo.y & 0xFFFF0000u)};
-      float b[4] = {__uint_as_float(hi.x << 16), __uint_as_float(hi.x & 0xFFFF0000u),
-                    __uint_as_float(hi.y << 16), __uint_as_float(hi.y & 0xFFFF0000u)};
+      float a[4] = {h_lo(lo.x), h_hi(lo.x),
+                    h_lo(lo.y), h_hi(lo.y)};
+      float b[4] = {h_lo(hi.x), h_hi(hi.x),
+                    h_lo(hi.y), h_hi(hi.y)};
       const float cc[4] = {c.x, c.y, c.z, c.w};
       const float ss[4] = {sn.x, sn.y, sn.z, sn.w};
       float ra[4], rb[4];
@@ -271,21 +271,21 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
         ra[j] = __fsub_rn(__fmul_rn(a[j], cc[j]), __fmul_rn(b[j], ss[j]));
         rb[j] = __fadd_rn(__fmul_rn(b[j], cc[j]), __fmul_rn(a[j], ss[j]));
       }
-      olo.x = pack2bf(ra[0], ra[1]); olo.y = pack2bf(ra[2], ra[3]);
-      ohi.x = pack2bf(rb[0], rb[1]); ohi.y = pack2bf(rb[2], rb[3]);
+      olo.x = pack2h(ra[0], ra[1]); olo.y = pack2h(ra[2], ra[3]);
+      ohi.x = pack2h(rb[0], rb[1]); ohi.y = pack2h(rb[2], rb[3]);
     } else {  // V: natural order, copied as is
-      const bf16_t* hp = row + head * kHeadDim;
+      const f16_t* hp = row + head * kHeadDim;
       olo = *(const uint2*)(hp + i0);
       ohi = *(const uint2*)(hp + i0 + 64);
     }
     if (head < Hq) {
-      bf16_t* hp = row + head * kHeadDim;
+      f16_t* hp = row + head * kHeadDim;
       *(uint2*)(hp + i0) = olo;
       *(uint2*)(hp + i0 + 64) = ohi;
     } else {
       const bool is_k = head < Hq + Hk;
       const int kh = is_k ? head - Hq : head - Hq - Hk;
-      bf16_t* dst = (is_k ? kv.k : kv.v) +
+      f16_t* dst = (is_k ? kv.k : kv.v) +
                     (((size_t)page * kv.n_kv_heads + kh) * kPage + off) * kHeadDim;
       *(uint2*)(dst + i0) = olo;
       *(uint2*)(dst + i0 + 64) = ohi;
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16_t* __restrict__ qkv, 
   }
 }
 
-void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
+void launch_rope_kv(f16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
                     KVView kv, hipStream_t s) {
   if (T <= 0) return;
@@ -359,12 +359,16 @@ __device__ __forceinline__ int limb_sum(uint64_t seed_h, int kind, int layer, in
          131070;
 }
 
-__device__ __forceinline__ bf16_t rne_bits(float f) {  // integer RNE, finite inputs only
+// the generator's values are bf16-rounded (integer RNE, finite inputs only), as oracle/synth.py
+// restates; the engine stores them as fp16 (exact for |v| >= 2^-17: a bf16 significand has 8
+// bits; smaller magnitudes are rounded to fp16's subnormal grid, as llama.cpp's F16 converter
+// would round them)
+__device__ __forceinline__ f16_t rne_bits(float f) {
   const uint32_t u = __float_as_uint(f);
-  return (bf16_t)((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+  return f2h(__uint_as_float((u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u));
 }
 
-__global__ void synth_linear_kernel(bf16_t* dst, int kind, int layer, int rows, int cols,
+__global__ void synth_linear_kernel(f16_t* dst, int kind, int layer, int rows, int cols,
                                     uint64_t seed_h, float scale, int map_mul, int map_add) {
   const size_t n = (size_t)rows * cols;
   for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -375,7 +379,7 @@ __global__ void synth_linear_kernel(bf16_t* dst, int kind, int layer, int rows, 
   }
 }
 
-__global__ void synth_norm_kernel(bf16_t* dst, int kind, int layer, int n, uint64_t seed_h,
+__global__ void synth_norm_kernel(f16_t* dst, int kind, int layer, int n, uint64_t seed_h,
                                   float scale) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < n; c += gridDim.x * blockDim.x) {
     const float v = __fadd_rn(1.0f, __fmul_rn((float)limb_sum(seed_h, kind, layer, 0, c), scale));
@@ -390,7 +394,7 @@ static uint64_t host_splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
+void launch_synth_linear(f16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
                          float std, int map_mul, int map_add, hipStream_t s) {
   // scale = float32(std*sqrt(3)/65536), computed in double then rounded once (as numpy does)
   const float scale = (float)((double)std * 1.7320508075688772 / 65536.0);
@@ -398,21 +402,21 @@ void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, u
                      cols, host_splitmix64(seed), scale, map_mul, map_add);
 }
 
-void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
+void launch_synth_norm(f16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
                        hipStream_t s) {
   const float scale = (float)((double)jitter / 131070.0);
   MS_LAUNCH(synth_norm_kernel, dim3(16), dim3(256), 0, s, dst, kind, layer, n,
                      host_splitmix64(seed), scale);
 }
 
-__global__ void scatter_rows_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__ dst,
+__global__ void scatter_rows_kernel(const f16_t* __restrict__ src, f16_t* __restrict__ dst,
                                     int rows, int cols, int map_mul, int map_add) {
   const int r = blockIdx.x;
   const size_t dr = map_row(r, map_mul, map_add);
   for (int c = threadIdx.x; c < cols; c += blockDim.x) dst[dr * cols + c] = src[(size_t)r * cols + c];
 }
 
-void launch_scatter_rows(const bf16_t* src, bf16_t* dst, int rows, int cols, int map_mul,
+void launch_scatter_rows(const f16_t* src, f16_t* dst, int rows, int cols, int map_mul,
                          int map_add, hipStream_t s) {
   MS_LAUNCH(scatter_rows_kernel, dim3(rows), dim3(256), 0, s, src, dst, rows, cols,
                      map_mul, map_add);

@@ -8,8 +8,8 @@
 // is bit-identical to the C restatement.
 //
 // Storage (engine.cpp): every quantised matrix keeps both
-//   * a bf16 copy = bf16_rne(dequant(blocks)) in the fused row layout, for prefill GEMMs
-//     and the embedding gather (compute-bound; bf16 is what MFMA consumes), and
+//   * a fp16 copy = f16(dequant(blocks)) in the fused row layout, for prefill GEMMs
+//     and the embedding gather (compute-bound; fp16 is what MFMA consumes), and
 //   * the quantised rows for decode, which is HBM-bound: 4.5 / 6.56 bits per weight
 //     instead of 16.  Q4_K blocks keep their 16-B ggml header (d, dmin, 12 scale bytes) and
 //     144 B, but the 128 quant bytes are re-ordered so that lane group g of a wave reads,
@@ -17,22 +17,24 @@
 //     q[k_i] | q[k_{i+4}] << 4); Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales
 //     16 | d 2 + pad] so every field is 16-B aligned.
 // The fused GEMV streams the blocks HBM -> VGPR (one super-block of 256 weights per row
-// per wave-step) and feeds v_mfma_f32_16x16x32_bf16:
-//   * Q4_K, one MFMA per 32-weight sub-block: the nibbles become bf16 (128 + q) by a byte
-//     permute against 0x43 (exact integers), the MFMA gives A_s = sum_k x_k (128 + q_k), and
-//     sum_k x_k y_k = d_s A_s - (128 d_s + m_s) X_s with d_s = d*sc_s, m_s = dmin*m_s (ggml's
+// per wave-step) and feeds v_mfma_f32_16x16x32_f16:
+//   * Q4_K, one MFMA per 32-weight sub-block: the nibbles become the fp16 subnormals q 2^-24
+//     by a byte permute (exact; gfx950 MFMA keeps fp16 denormal operands), the MFMA gives
+//     A_s = 2^-24 sum_k x_k q_k, and sum_k x_k y_k = (2^24 d_s) A_s - m_s X_s with d_s = d*sc_s,
+//     m_s = dmin*m_s (ggml's
 //     fp32 d1 / m1) and X_s = sum of the sub-block's x (one more MFMA, against ones, shared
 //     by the weight tiles of the block) -- 2 FMAs per output
 //     element per sub-block instead of dequantising every weight: the decode GEMV uses the
-//     exact fp32 dequantised weights (no bf16 rounding of them);
-//   * Q6_K, dequantised in registers to the bf16 values of the bf16 copy.
+//     exact fp32 dequantised weights (no fp16 rounding of them, and no cancellation: a
+//     1024 + q bias form cost ~7e-6 relative against fp64);
+//   * Q6_K, dequantised in registers to the fp16 values of the fp16 copy.
 #include <cstdlib>
 
 #include "gemv_common.h"
 
 namespace ms {
 
-__device__ __forceinline__ float h2f(uint32_t h16) {
+__device__ __forceinline__ float h2f_lo(uint32_t h16) {
   return (float)__builtin_bit_cast(_Float16, (uint16_t)(h16 & 0xFFFFu));
 }
 
@@ -57,7 +59,7 @@ __device__ __forceinline__ void scale_min_k4(const uint4& hdr, int j, int& d, in
 // one 256-thread block per super-block, thread t -> weight t (the C loop order)
 __device__ __forceinline__ float deq_q4k_one(const uint8_t* b, int t) {
   const uint4 hdr = *(const uint4*)b;
-  const float d = h2f(hdr.x), dmin = h2f(hdr.x >> 16);
+  const float d = h2f_lo(hdr.x), dmin = h2f_lo(hdr.x >> 16);
   const int c = t >> 6, w = t & 63, h = w >> 5, l = w & 31;
   int sc, m;
   scale_min_k4(hdr, 2 * c + h, sc, m);
@@ -74,7 +76,7 @@ __device__ __forceinline__ float deq_q6k_one(const uint8_t* b, int t) {
   const uint32_t hb = b[128 + n * 32 + l];
   const int q = (int)(((k4 >> 1) ? (a >> 4) : (a & 0xF)) | (((hb >> (2 * k4)) & 3) << 4)) - 32;
   const int sc = (int)(int8_t)b[192 + n * 8 + (l >> 4) + 2 * k4];
-  const float d = h2f((uint32_t)b[208] | ((uint32_t)b[209] << 8));
+  const float d = h2f_lo((uint32_t)b[208] | ((uint32_t)b[209] << 8));
   return __fmul_rn(__fmul_rn(d, (float)sc), (float)q);
 }
 
@@ -92,9 +94,9 @@ void launch_dequant_f32(int type, const uint8_t* blocks, int64_t n_blocks, float
   MS_LAUNCH(dequant_f32_kernel, dim3((unsigned)n_blocks), dim3(256), 0, s, type, blocks, out);
 }
 
-// rows of raw blocks -> (a) bf16 rows of the fused matrix, (b) packed quantised rows
+// rows of raw blocks -> (a) fp16 rows of the fused matrix, (b) packed quantised rows
 __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t* __restrict__ blocks,
-                                                         int K, bf16_t* __restrict__ dst_bf16,
+                                                         int K, f16_t* __restrict__ dst_f16,
                                                          int map_mul, int map_add,
                                                          uint8_t* __restrict__ dst_q, int q_row_base) {
   const int r = blockIdx.y, sb = blockIdx.x, t = threadIdx.x;
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
   const uint8_t* b = blocks + ((size_t)r * nsb + sb) * braw;
   const float y = (type == MS_QT_Q4_K) ? deq_q4k_one(b, t) : deq_q6k_one(b, t);
   const size_t drow = map_row(r, map_mul, map_add);
-  dst_bf16[drow * K + (size_t)sb * 256 + t] = f2bf(y);
+  dst_f16[drow * K + (size_t)sb * 256 + t] = f2h(y);
   if (dst_q) {
     const int bp = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KPacked;
     uint8_t* q = dst_q + ((drow - q_row_base) * nsb + sb) * bp;
@@ -126,10 +128,10 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
   }
 }
 
-void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t* dst_bf16, int map_mul,
+void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, f16_t* dst_f16, int map_mul,
                        int map_add, uint8_t* dst_q, int q_row_base, hipStream_t s) {
   if (rows <= 0) return;
-  MS_LAUNCH(quant_rows_kernel, dim3(K / 256, rows), dim3(256), 0, s, type, blocks, K, dst_bf16,
+  MS_LAUNCH(quant_rows_kernel, dim3(K / 256, rows), dim3(256), 0, s, type, blocks, K, dst_f16,
             map_mul, map_add, dst_q, q_row_base);
 }
 
@@ -185,7 +187,7 @@ void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t 
 // same k -- a k permutation applied to both operands, so every dot product is unchanged.
 // XM: the X source (gemv_common.h kXGlobal / kXLds / kXRegs, as in k_gemv.hip)
 template <int MT, int NT, int EPI, int SBW, int XM, bool RS>
-__global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ X, QMat qm,
+__global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X, QMat qm,
                                                      void* __restrict__ out, int M, int N, int K,
                                                      int ldo, int rinv_off, GemvArgs ga) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
   if constexpr (XL) gemv_dma_x(smem, X, M, K, ldx);
   // Q4_K sub-block s of super-block j: lane group g's 8 weights at k = (j*8 + s)*32 + 8g;
   // Q6_K MFMA t: k = j*256 + hh*128 + (t>>1)*32 + 16p + 8(t&1)
-  bf16x8 xr[XR ? SBW : 1][XR ? 8 : 1][XR ? MT : 1];
+  f16x8 xr[XR ? SBW : 1][XR ? 8 : 1][XR ? MT : 1];
   if constexpr (XR) {
     const bool q6 = type != MS_QT_Q4_K;
 #pragma unroll
@@ -231,7 +233,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
         for (int m = 0; m < MT; ++m) {
           const int k = q6 ? (sb0 + j) * 256 + (g >> 1) * 128 + (t >> 1) * 32 + 16 * (g & 1) + 8 * (t & 1)
                            : ((sb0 + j) * 8 + t) * 32 + 8 * g;
-          xr[j][t][m] = as_bf16x8(ldg16(X + (size_t)min(m * 16 + fr, M - 1) * ldx + k));
+          xr[j][t][m] = as_f16x8(ldg16(X + (size_t)min(m * 16 + fr, M - 1) * ldx + k));
         }
   }
   __builtin_amdgcn_sched_barrier(0);
@@ -252,7 +254,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
       __builtin_amdgcn_s_barrier();  // no fence: a fence would wait for the weight loads too
     }
     typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-    const bf16x8 ones = __builtin_bit_cast(bf16x8, u4v{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+    const f16x8 ones = __builtin_bit_cast(f16x8, u4v{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u});
 #pragma unroll
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
@@ -262,9 +264,9 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
           const int xrow = min(m * 16 + fr, M - 1);
-          const bf16x8 xf = XR ? xr[XR ? j : 0][XR ? s_ : 0][XR ? m : 0]
-                          : XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
-                               : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
+          const f16x8 xf = XR ? xr[XR ? j : 0][XR ? s_ : 0][XR ? m : 0]
+                          : XL ? *(const f16x8*)(smem + x_lds(xrow, k, K))
+                               : *(const f16x8*)(X + (size_t)xrow * ldx + k);
           // X_s = the sub-block's sum of each row's x: one more MFMA against ones, shared by
           // the NT weight tiles (no separate pass over X, no barrier)
           const f32x4 xs = mfma16(xf, ones, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -274,21 +276,20 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
             const uint4 h = hq[j][n];
             const uint32_t scw = s_ < 4 ? (h.y & 0x3F3F3F3Fu) : ((h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u));
             const uint32_t mw = s_ < 4 ? (h.z & 0x3F3F3F3Fu) : (((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u));
-            const float d1 = __fmul_rn(h2f(h.x), (float)((scw >> sh) & 0xFFu));        // ggml d1 = d * sc
-            const float m1 = __fmul_rn(h2f(h.x >> 16), (float)((mw >> sh) & 0xFFu));   // ggml m1 = dmin * m
-            const float c1 = __fmaf_rn(128.0f, d1, m1);                          // 128 d1 + m1 (exact 128 d1)
+            const float d1 = __fmul_rn(h2f_lo(h.x), (float)((scw >> sh) & 0xFFu));        // ggml d1 = d * sc
+            const float m1 = __fmul_rn(h2f_lo(h.x >> 16), (float)((mw >> sh) & 0xFFu));   // ggml m1 = dmin * m
+            const float d1s = d1 * 16777216.0f;                                  // d1 * 2^24 (exact)
             const uint4 qq = s_ < 4 ? q0[j][n] : q1[j][n];
             const int si = s_ & 3;
             const uint32_t qw = si == 0 ? qq.x : si == 1 ? qq.y : si == 2 ? qq.z : qq.w;
             const uint32_t lo = qw & 0x0F0F0F0Fu, hi = (qw >> 4) & 0x0F0F0F0Fu;
-            // bytes [q, 0x43, q', 0x43] = bf16 (128 + q, 128 + q'): weights k .. k+7 in order
-            const u4v pk = {__builtin_amdgcn_perm(0x43434343u, lo, 0x04010400u),
-                            __builtin_amdgcn_perm(0x43434343u, lo, 0x04030402u),
-                            __builtin_amdgcn_perm(0x43434343u, hi, 0x04010400u),
-                            __builtin_amdgcn_perm(0x43434343u, hi, 0x04030402u)};
-            const f32x4 A = mfma16(xf, __builtin_bit_cast(bf16x8, pk), f32x4{0.f, 0.f, 0.f, 0.f});
+            // bytes [q, 0, q', 0] = the fp16 subnormals q * 2^-24, q' * 2^-24 (exact): weights
+            // k .. k+7 in order (perm selector 0x0C is the constant byte 0)
+            const u4v pk = {__builtin_amdgcn_perm(0u, lo, 0x0C010C00u), __builtin_amdgcn_perm(0u, lo, 0x0C030C02u),
+                            __builtin_amdgcn_perm(0u, hi, 0x0C010C00u), __builtin_amdgcn_perm(0u, hi, 0x0C030C02u)};
+            const f32x4 A = mfma16(xf, __builtin_bit_cast(f16x8, pk), f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[m][n][i] = __fmaf_rn(-c1, xs[i], __fmaf_rn(d1, A[i], acc[m][n][i]));
+            for (int i = 0; i < 4; ++i) acc[m][n][i] = __fmaf_rn(-m1, xs[i], __fmaf_rn(d1s, A[i], acc[m][n][i]));
           }
         }
       }
@@ -316,7 +317,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const float d = h2f(dw[j][n]);
+        const float d = h2f_lo(dw[j][n]);
 #pragma unroll
         for (int t = 0; t < 8; ++t) {
           const int k4 = t >> 1, sub = t & 1;
@@ -339,17 +340,17 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const bf16_t* __restrict__ 
             const f2 ds2 = {ds, ds}, nds2 = {nds, nds};  // two weights per v_pk_fma_f32
             const f2 y01 = __builtin_elementwise_fma(ds2, f2{(float)(q4 & 0xFFu), (float)((q4 >> 8) & 0xFFu)}, nds2);
             const f2 y23 = __builtin_elementwise_fma(ds2, f2{(float)((q4 >> 16) & 0xFFu), (float)(q4 >> 24)}, nds2);
-            pk[2 * w] = pack2bf(y01.x, y01.y);
-            pk[2 * w + 1] = pack2bf(y23.x, y23.y);
+            pk[2 * w] = pack2h(y01.x, y01.y);
+            pk[2 * w + 1] = pack2h(y23.x, y23.y);
           }
-          const bf16x8 wf = __builtin_bit_cast(bf16x8, pk);
+          const f16x8 wf = __builtin_bit_cast(f16x8, pk);
           const int k = (sb0 + j) * 256 + hh * 128 + k4 * 32 + 16 * p + 8 * sub;
 #pragma unroll
           for (int m = 0; m < MT; ++m) {
             const int xrow = min(m * 16 + fr, M - 1);
-            const bf16x8 xf = XR ? xr[XR ? j : 0][XR ? t : 0][XR ? m : 0]
-                            : XL ? *(const bf16x8*)(smem + x_lds(xrow, k, K))
-                                 : *(const bf16x8*)(X + (size_t)xrow * ldx + k);
+            const f16x8 xf = XR ? xr[XR ? j : 0][XR ? t : 0][XR ? m : 0]
+                            : XL ? *(const f16x8*)(smem + x_lds(xrow, k, K))
+                                 : *(const f16x8*)(X + (size_t)xrow * ldx + k);
             acc[m][n] = mfma16(xf, wf, acc[m][n]);
           }
         }
@@ -409,7 +410,7 @@ bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles) {
 }
 
 template <int MT, int NT, int EPI>
-static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
+static void qgemv_go(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo,
                      const QPlan& p, const GemvArgs& ga_in, hipStream_t s, int S = 1) {
   GemvArgs ga = ga_in;
   if (EPI == MS_GEMV_EPI_ARGMAX || EPI == MS_GEMV_EPI_ADD_F32) ga.rs = RowScale{};  // r > 0 keeps the order
@@ -444,10 +445,10 @@ static void qgemv_go(const bf16_t* X, const QMat& q, void* out, int M, int N, in
 }
 
 template <int MT>
-static void qgemv_go_mt(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+static void qgemv_go_mt(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                         const QPlan& p, const GemvArgs& ga, hipStream_t s) {
   switch (epi) {
-    case MS_GEMV_EPI_STORE_BF16: qgemv_go<MT, 1, MS_GEMV_EPI_STORE_BF16>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    case MS_GEMV_EPI_STORE_F16: qgemv_go<MT, 1, MS_GEMV_EPI_STORE_F16>(X, q, out, M, N, K, ldo, p, ga, s); break;
     case MS_GEMV_EPI_ADD_F32: qgemv_go<MT, 1, MS_GEMV_EPI_ADD_F32>(X, q, out, M, N, K, ldo, p, ga, s); break;
     case MS_GEMV_EPI_SWIGLU: qgemv_go<MT, 2, MS_GEMV_EPI_SWIGLU>(X, q, out, M, N, K, ldo, p, ga, s); break;
     case MS_GEMV_EPI_ROPE_KV: qgemv_go<MT, 1, MS_GEMV_EPI_ROPE_KV>(X, q, out, M, N, K, ldo, p, ga, s); break;
@@ -456,7 +457,7 @@ static void qgemv_go_mt(const bf16_t* X, const QMat& q, void* out, int M, int N,
   }
 }
 
-void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga_in, hipStream_t s) {
   if (M <= 0) return;
   const QPlan p = qplan(M, N, K, epi);
@@ -478,7 +479,7 @@ bool qgemv_split_supported(int M, int N, int K, int S, int rs_tiles) {
 
 // fp32 partial slabs [S][M][N] over S equal K ranges (super-block aligned); the caller
 // folds them (residual_rmsnorm_kernel / the decode attention prologue)
-void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
+void launch_qgemv_split(const f16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
                         hipStream_t s, const GemvArgs* ga_in) {
   if (M <= 0) return;
   const int Ks = K / S;

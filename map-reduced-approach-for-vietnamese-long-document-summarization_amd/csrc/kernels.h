@@ -4,10 +4,10 @@
 
 namespace ms {
 
-// Where the K/V of one layer live: pool[page][kv_head][64 tokens][128] bf16.
+// Where the K/V of one layer live: pool[page][kv_head][64 tokens][128] fp16.
 struct KVView {
-  bf16_t* k;
-  bf16_t* v;
+  f16_t* k;
+  f16_t* v;
   const int32_t* block_table;  // [slots][max_pages]
   int32_t max_pages;           // row stride of block_table
   int32_t n_kv_heads;
@@ -17,12 +17,13 @@ struct KVView {
 };
 
 // Prefill attention work description (device arrays, see engine.cpp StepArgs).
+constexpr int kPrefillQRows = 128;  // query rows per prefill attention block (8 waves x 16)
 struct PrefillAttnArgs {
   const int32_t* seq_qstart;  // [S] row of the sequence's first query token in qkv
   const int32_t* seq_qlen;    // [S]
   const int32_t* seq_kvlen;   // [S] keys visible to the last query (= cached + qlen)
   const int32_t* seq_slot;    // [S] block-table row
-  const int32_t* qblk;        // [NQB] (seq << 16) | q_block, heaviest first
+  const int32_t* qblk;        // [NQB] (seq << 16) | q_block (kPrefillQRows rows), heaviest first
   int32_t n_qblk;
 };
 
@@ -35,7 +36,7 @@ struct DecodeAttnArgs {
 };
 
 // The deferred RMSNorm of the numerics contract (oracle/llama_ref.py): a
-// normalised projection (QKV, gate/up, lm_head) multiplies the bf16 GEMM input bf16(x * g) by
+// normalised projection (QKV, gate/up, lm_head) multiplies the fp16 GEMM input f16(x * g) by
 // W and scales output row r by rinv(r) = rsq(sum_t ssq[t][r] / H + eps), where ssq holds
 // partial sums of x[r]^2 [tiles][rows] written by the producer of x (a norm kernel: one tile;
 // a RESID_SSQ GEMV epilogue: one per column tile).  Every consumer forms the sum in the same
@@ -57,36 +58,36 @@ __device__ __forceinline__ float rs_rinv(float sum, const RowScale& rs) {
   return __builtin_amdgcn_rsqf(__fmaf_rn(sum, rs.inv_h, rs.eps));
 }
 
-// x = the embedding rows; with gamma also xg = bf16(x * gamma) and ssq = per-row sums of x^2
+// x = the embedding rows; with gamma also xg = f16(x * gamma) and ssq = per-row sums of x^2
 // (the first normalised projection's input, one-tile RowScale)
-void launch_embed(const int32_t* ids, int T, const bf16_t* emb, int H, float* x, hipStream_t s,
-                  const bf16_t* gamma = nullptr, bf16_t* xg = nullptr, float* ssq = nullptr);
+void launch_embed(const int32_t* ids, int T, const f16_t* emb, int H, float* x, hipStream_t s,
+                  const f16_t* gamma = nullptr, f16_t* xg = nullptr, float* ssq = nullptr);
 // chained decode: next ids <- this step's argmax (clamped into [0, V)), positions and key
 // counts += 1 in the step-argument blob [ids | positions | slots | key counts | step], and the
 // raw ids appended to ring row `step` (B <= 256)
 void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring, int B, int V,
                            hipStream_t s);
-// the GEMM input of a normalised projection: y[r] = bf16(x[row_idx[r]] * w), ssq[r] = sum of
+// the GEMM input of a normalised projection: y[r] = f16(x[row_idx[r]] * w), ssq[r] = sum of
 // x[row_idx[r]]^2 (one-tile RowScale); row_idx optional (gather)
-void launch_rmsnorm(const float* x, const bf16_t* w, bf16_t* y, float* ssq, int rows, int H,
+void launch_rmsnorm(const float* x, const f16_t* w, f16_t* y, float* ssq, int rows, int H,
                     const int32_t* row_idx, hipStream_t s);
 // RoPE on Q (in place, rope-permuted -> natural dim order) and K; K,V scattered into the
 // paged cache.  Q/K heads arrive in the rope-permuted row order of the fused weights.
-void launch_rope_kv(bf16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
+void launch_rope_kv(f16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
                     KVView kv, hipStream_t s);
 void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s);
 
-// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 bf16, K % 64 == 0; rs (one tile, or null):
+// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 fp16, K % 64 == 0; rs (one tile, or null):
 // the deferred RMSNorm scale of the output rows (epilogues 0, 2, 3)
-void launch_gemm(const bf16_t* A, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, hipStream_t s, const RowScale* rs = nullptr);
 // tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
 void set_gemm_variant(int v);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {
-  MS_GEMV_EPI_STORE_BF16 = 0,
+  MS_GEMV_EPI_STORE_F16 = 0,
   MS_GEMV_EPI_ADD_F32 = 1,
   MS_GEMV_EPI_SWIGLU = 2,
   MS_GEMV_EPI_STORE_F32 = 3,
@@ -96,7 +97,7 @@ enum {
   MS_GEMV_EPI_ARGMAX = 5,
   // residual update + the next RMSNorm's inputs (decode O / down, no split-K): out = x fp32
   // [M][ldo], x[r][c] += acc; ga.ssq_out[tile][r] = sum over the tile's columns of the new
-  // x[r][c]^2 (a fixed lane tree) and ga.xg_out[r][c] = bf16(x[r][c] * ga.gamma[c]): the next
+  // x[r][c]^2 (a fixed lane tree) and ga.xg_out[r][c] = f16(x[r][c] * ga.gamma[c]): the next
   // projection's GEMM input and its deferred row scale (RowScale), with no norm launch
   MS_GEMV_EPI_RESID_SSQ = 6
 };
@@ -112,11 +113,11 @@ struct GemvArgs {
   // exactly 256 workgroups (one per CU) without split-K
   int rt;
   // RESID_SSQ epilogue: per-tile sums of squares [tiles][M], the next norm's gain [ldo] and
-  // the bf16 GEMM input it feeds [M][ldo]
+  // the fp16 GEMM input it feeds [M][ldo]
   float* ssq_out;
-  const bf16_t* gamma;
-  bf16_t* xg_out;
-  // deferred RMSNorm scale of the output rows (STORE_BF16 / STORE_F32 / SWIGLU / ROPE_KV /
+  const f16_t* gamma;
+  f16_t* xg_out;
+  // deferred RMSNorm scale of the output rows (STORE_F16 / STORE_F32 / SWIGLU / ROPE_KV /
   // ARGMAX epilogues)
   RowScale rs;
 };
@@ -126,35 +127,35 @@ bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);
 // whether a decode GEMV / Q-GEMV can take a deferred-norm scale of `tiles` partial sums per row
 // (staged in LDS: tiles * M <= 4096)
 bool gemv_rs_supported(int M, int tiles);
-void launch_gemv_split(const bf16_t* X, const bf16_t* W, float* slabs, int M, int N, int K, int S,
+void launch_gemv_split(const f16_t* X, const f16_t* W, float* slabs, int M, int N, int K, int S,
                        int force_waves, hipStream_t s, const GemvArgs* ga = nullptr);
 // X [M][ldk] and W [N][ldk] rows of stride ldk >= K (tuning hook: padded weight layouts)
-void launch_gemv_strided(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldk,
+void launch_gemv_strided(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldk,
                          int ldo, int epi, hipStream_t s);
 // rows of {max, id} partials [rows][tiles] -> ids (-1: no finite maximum)
 void launch_argmax_partials(const void* partials, int rows, int tiles, int32_t* out, hipStream_t s);
 
-// x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = bf16(x * w)
+// x[r] += slab[0][r] + ... + slab[S-1][r] (left to right, then added to x); y = f16(x * w)
 // and ssq[r] = sum of x[r]^2 (the one-tile RowScale of the projection y feeds).  S = 0: no
 // slabs.  Supported: S <= 8, H <= 3072 (H > 3072 only with S = 0).
 bool residual_rmsnorm_supported(int S, int H);
-void launch_residual_rmsnorm(float* x, const float* slabs, int S, const bf16_t* w, bf16_t* y,
+void launch_residual_rmsnorm(float* x, const float* slabs, int S, const f16_t* w, f16_t* y,
                              float* ssq, int rows, int H, hipStream_t s);
 size_t gemv_workspace_bytes(int M, int N, int K);
 // rs_tiles > 0: the call carries deferred-norm statistics of that many tiles (RowScale), which
 // the staged-partials LDS and kRsStage must also fit
 bool gemv_supported(int M, int N, int K, int epi, int rs_tiles = 0);
-void launch_gemv(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+void launch_gemv(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, void* ws, hipStream_t s);
 // ga: prologue/epilogue arguments (or null); force_waves: tuning hook (0 = heuristic)
-void launch_gemv_ex(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int ldo,
+void launch_gemv_ex(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int ldo,
                     int epi, const GemvArgs* ga, int force_waves, hipStream_t s);
 
 // large-batch decode projections (k_dgemm.hip): 64 weight rows x all M <= 256 rows per block,
 // X shared through LDS; S > 1 = split-K fp32 slabs [S][M][N] (STORE_F32 only).  Epilogues as
 // the GEMV's except ROPE_KV; N % 64 == 0, K % (64 S) == 0.
 bool dgemm_supported(int M, int N, int K, int S, int epi);
-void launch_dgemm(const bf16_t* X, const bf16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+void launch_dgemm(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
                   hipStream_t s, const RowScale* rs = nullptr);
 
 // ---- ggml K-quant weights (k_qgemv.hip)
@@ -178,28 +179,28 @@ inline int qblock_bytes(int type, bool packed) {
   return type == MS_QT_Q4_K ? kQ4KBytes : (packed ? kQ6KPacked : kQ6KBytes);
 }
 void launch_dequant_f32(int type, const uint8_t* blocks, int64_t n_blocks, float* out, hipStream_t s);
-// raw ggml rows [rows][K/256 blocks] -> bf16 rows of a fused matrix (map_row) and, if dst_q,
+// raw ggml rows [rows][K/256 blocks] -> fp16 rows of a fused matrix (map_row) and, if dst_q,
 // packed quantised rows at (map_row(r) - q_row_base)
-void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, bf16_t* dst_bf16,
+void launch_quant_rows(int type, const uint8_t* blocks, int rows, int K, f16_t* dst_f16,
                        int map_mul, int map_add, uint8_t* dst_q, int q_row_base, hipStream_t s);
 void launch_synth_qblocks(int type, uint8_t* blocks, int64_t n_blocks, uint64_t seed, float scale,
                           hipStream_t s);
 bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles = 0);
 bool qgemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);
-void launch_qgemv_split(const bf16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
+void launch_qgemv_split(const f16_t* X, const QMat& q, float* slabs, int M, int N, int K, int S,
                         hipStream_t s, const GemvArgs* ga = nullptr);
-void launch_qgemv(const bf16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
+void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga, hipStream_t s);
 
-void launch_attn_prefill(const bf16_t* qkv, bf16_t* out, int Hq, int Hk, KVView kv,
+void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s);
-// decode attention input: either bf16 qkv rows already roped with K/V in the cache
+// decode attention input: either fp16 qkv rows already roped with K/V in the cache
 // (slabs == nullptr), or S fp32 split-K slabs of the QKV projection (rope-permuted Q/K rows):
 // the kernel then adds the slabs, applies RoPE and writes the new token's K/V itself.
 // With slabs, rs is the deferred RMSNorm scale of the QKV rows (tiles <= 256): the kernel
-// rounds q/k/v = bf16(rinv(b) * sum of the slabs).
+// rounds q/k/v = f16(rinv(b) * sum of the slabs).
 struct DecodeQKV {
-  const bf16_t* qkv;
+  const f16_t* qkv;
   const float* slabs;
   int S;
   const float* cos_tab;
@@ -212,7 +213,7 @@ bool attn_decode_supported(int B, int Hq, int Hk, int max_len);
 // pages per wave of an engine's decode attention (from its max_batch / max_ctx, never from
 // one step's batch: the split boundaries set a sequence's summation order)
 int attn_decode_ppw(int max_batch, int Hk, int max_ctx);
-void launch_attn_decode(const DecodeQKV& qa, bf16_t* out, int Hq, int Hk, KVView kv,
+void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv,
                         DecodeAttnArgs a, float* ws, hipStream_t s);
 
 // synthetic weights (oracle/synth.py restates this generator)
@@ -225,12 +226,12 @@ __host__ __device__ inline size_t map_row(int r, int map_mul, int map_add) {
   if (map_mul == 0) return (size_t)(r & ~127) + rope_perm(r & 127) + map_add;
   return (size_t)(r >> 4) * map_mul + (r & 15) + map_add;
 }
-void launch_synth_linear(bf16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
+void launch_synth_linear(f16_t* dst, int kind, int layer, int rows, int cols, uint64_t seed,
                          float std, int map_mul, int map_add, hipStream_t s);
-void launch_synth_norm(bf16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
+void launch_synth_norm(f16_t* dst, int kind, int layer, int n, uint64_t seed, float jitter,
                        hipStream_t s);
 // scatter a logical [rows][cols] tensor into a fused/interleaved physical layout
-void launch_scatter_rows(const bf16_t* src, bf16_t* dst, int rows, int cols, int map_mul,
+void launch_scatter_rows(const f16_t* src, f16_t* dst, int rows, int cols, int map_mul,
                          int map_add, hipStream_t s);
 
 }  // namespace ms

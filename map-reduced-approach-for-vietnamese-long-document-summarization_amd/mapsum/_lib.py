@@ -13,13 +13,13 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # MAPSUM_LIB: an alternative in-tree build of the same library (A/B timing of build variants)
 LIB_PATH = os.environ.get("MAPSUM_LIB") or os.path.join(_HERE, "libmapsum.so")
 
-MS_ABI_VERSION = 2
+MS_ABI_VERSION = 3
 MS_OK, MS_EIO, MS_ENOMEM, MS_EBUSY, MS_EINVAL, MS_ENOSPC = 0, -5, -12, -16, -22, -28
 MS_FINISH_EOS, MS_FINISH_LENGTH, MS_FINISH_ERROR = 1, 2, 3
 MS_FLAG_IGNORE_EOS = 1
 (MS_T_EMBED, MS_T_ATTN_NORM, MS_T_WQ, MS_T_WK, MS_T_WV, MS_T_WO, MS_T_FFN_NORM, MS_T_WGATE,
  MS_T_WUP, MS_T_WDOWN, MS_T_FINAL_NORM, MS_T_LM_HEAD) = range(12)
-MS_EPI_STORE_BF16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
+MS_EPI_STORE_F16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
 MS_EPI_ARGMAX = 5
 MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms

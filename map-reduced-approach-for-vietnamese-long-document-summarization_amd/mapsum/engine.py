@@ -170,8 +170,9 @@ class Engine(RequestQueue):
     def declare_weight_q(self, tensor: int, layer: int, ggml_type: int):
         self._chk(self.lib.ms_declare_weight_q(self.h, tensor, layer, ggml_type), "ms_declare_weight_q")
 
-    def load_tensor(self, tensor: int, layer: int, bf16_bits: np.ndarray):
-        a = np.ascontiguousarray(bf16_bits, dtype=np.uint16)
+    def load_tensor(self, tensor: int, layer: int, f16_bits: np.ndarray):
+        """Upload one logical tensor as IEEE fp16 bit patterns (mapsum.weights.f32_to_f16_bits)."""
+        a = np.ascontiguousarray(f16_bits, dtype=np.uint16)
         self._chk(self.lib.ms_load_weight(self.h, tensor, layer, a.ctypes.data, a.size), "ms_load_weight")
 
     def set_eos_ids(self, ids):

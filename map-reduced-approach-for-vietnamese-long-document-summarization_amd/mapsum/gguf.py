@@ -12,8 +12,8 @@ The kernels implement HF's rotate-half convention, so those rows are put back he
 row of a quantised matrix is a whole run of blocks, so the same row permutation applies
 to Q4_K / Q6_K data without dequantising.
 
-Supported: every matrix float (F32 / F16 / BF16, uploaded as bf16 -- F16 values outside
-bf16's 8-bit mantissa are rounded) or every matrix Q4_K / Q6_K (the
+Supported: every matrix float (F32 / F16 / BF16, uploaded as fp16 -- the engine's type, so an
+F16 file such as llama3.2:3b-instruct-fp16 loads bit for bit) or every matrix Q4_K / Q6_K (the
 Q4_K_M mix) with float norms.
 """
 from __future__ import annotations

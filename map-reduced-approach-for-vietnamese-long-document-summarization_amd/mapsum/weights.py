@@ -2,7 +2,7 @@
 
 Sources:
   * a logical weight dict (``oracle.synth.make_weights`` layout: float32 arrays holding
-    bf16 values) -- used by the parity tests;
+    bf16 values, which fp16 holds exactly) -- used by the parity tests;
   * a Hugging Face Llama-3.2 checkpoint directory (``*.safetensors``; rotate-half RoPE
     convention, which is what the kernels implement) -- the real-weight path.  The
     reference pulls ``llama3.2:3b`` through Ollama (README.md:28-33); its GGUF blobs load
@@ -20,16 +20,16 @@ import numpy as np
 from . import _lib as L
 
 
-def f32_to_bf16_bits(a: np.ndarray) -> np.ndarray:
-    """Round-to-nearest-even float32 -> bf16 bit patterns (uint16)."""
-    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32)
-    return ((u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16)).astype(np.uint16)
+def f32_to_f16_bits(a: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even float32 -> IEEE fp16 bit patterns (uint16): the engine's weight
+    type (include/mapsum.h ms_load_weight), as llama.cpp's F16 GGUF converter rounds them."""
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32).astype(np.float16)).view(np.uint16)
 
 
 def load_logical(engine, w: dict):
     """Upload a logical weight dict ({embed, final_norm, lm_head, layers[...]})."""
     cfg = engine.cfg
-    up = lambda t, l, a: engine.load_tensor(t, l, f32_to_bf16_bits(a))  # noqa: E731
+    up = lambda t, l, a: engine.load_tensor(t, l, f32_to_f16_bits(a))  # noqa: E731
     up(L.MS_T_EMBED, 0, w["embed"])
     up(L.MS_T_FINAL_NORM, 0, w["final_norm"])
     if not cfg.tie_embeddings:
@@ -59,10 +59,10 @@ def load_quantized(engine, qw: dict, norms: dict):
     for key, (qt, blocks) in qw.items():
         layer, name = (0, key) if isinstance(key, str) else key
         engine.load_tensor_q(_Q_NAMES[name], layer, qt, blocks)
-    engine.load_tensor(L.MS_T_FINAL_NORM, 0, f32_to_bf16_bits(norms["final_norm"]))
+    engine.load_tensor(L.MS_T_FINAL_NORM, 0, f32_to_f16_bits(norms["final_norm"]))
     for i, ly in enumerate(norms["layers"]):
-        engine.load_tensor(L.MS_T_ATTN_NORM, i, f32_to_bf16_bits(ly["attn_norm"]))
-        engine.load_tensor(L.MS_T_FFN_NORM, i, f32_to_bf16_bits(ly["ffn_norm"]))
+        engine.load_tensor(L.MS_T_ATTN_NORM, i, f32_to_f16_bits(ly["attn_norm"]))
+        engine.load_tensor(L.MS_T_FFN_NORM, i, f32_to_f16_bits(ly["ffn_norm"]))
     if len([k for k in qw if not isinstance(k, str)]) != 7 * cfg.n_layers:
         raise RuntimeError("quantised model is missing per-layer matrices")
 
@@ -84,12 +84,12 @@ def _bits(t) -> np.ndarray:
     try:
         import torch
         if isinstance(t, torch.Tensor):
-            if t.dtype == torch.bfloat16:
+            if t.dtype == torch.float16:
                 return t.contiguous().view(torch.int16).numpy().view(np.uint16)
-            return f32_to_bf16_bits(t.float().numpy())
+            return f32_to_f16_bits(t.float().numpy())
     except ImportError:  # pragma: no cover
         pass
-    return f32_to_bf16_bits(np.asarray(t, dtype=np.float32))
+    return f32_to_f16_bits(np.asarray(t, dtype=np.float32))
 
 
 def load_hf_state_dict(engine, sd: dict):

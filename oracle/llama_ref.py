@@ -10,15 +10,16 @@ public Llama-3.2 one (RMSNorm, GQA attention with llama3-scaled rotate-half
 RoPE, SwiGLU MLP, tied lm_head) and is pinned against
 ``transformers.LlamaForCausalLM`` by ``tests/golden/make_golden.py``.
 
-Rounding points (the engine's numerics contract):
-  residual stream fp32; every GEMM input bf16, fp32 accumulate; a normalised projection
-  (QKV, gate/up, lm_head) multiplies bf16(x * g) by W and scales each output row by the
-  RMSNorm factor r = 1/sqrt(mean(x^2) + eps) in fp32 -- r * (bf16(x*g) . W^T), the
-  deferred form of W . (x*r*g), so the producer of x can emit the GEMM input without
-  knowing the row's norm; Q/K/V, RoPE output, attention output and the SwiGLU product
-  rounded to bf16; attention scores/softmax fp32; logits fp32; argmax ties -> lowest id.
-The only deliberate difference from the HIP path: softmax here is exact fp32 (the flash
-kernels feed P to the P.V MFMAs as hi + lo bf16 halves), which the tests' tolerances cover.
+Rounding points (the engine's numerics contract; mode "engine"):
+  weights fp16; residual stream fp32; every GEMM input fp16, fp32 accumulate; a normalised
+  projection (QKV, gate/up, lm_head) multiplies f16(x * g) by W and scales each output row by
+  the RMSNorm factor r = 1/sqrt(mean(x^2) + eps) in fp32 -- r * (f16(x*g) . W^T), the deferred
+  form of W . (x*r*g), so the producer of x can emit the GEMM input without knowing the row's
+  norm; Q/K/V, RoPE output, attention output and the SwiGLU product rounded to fp16; attention
+  scores/softmax fp32 with the probabilities rounded to fp16 for P.V; logits fp32; argmax
+  ties -> lowest id.  The flash kernels' online softmax takes each row's max per tile (and the
+  decode split combine per split), so their P rounding is not bit-identical to this one-pass
+  softmax; the tests' tolerances cover that.
 """
 from __future__ import annotations
 
@@ -110,13 +111,18 @@ def silu(x):
 class OracleLlama:
     """Greedy Llama-3.2 over bf16-valued float32 weights (oracle.synth.make_weights layout)."""
 
-    MODES = ("bf16", "fp32", "f16")
+    MODES = ("engine", "bf16", "fp32", "f16")
 
-    def __init__(self, cfg, weights: dict, round_bf16: bool = True, mode: str | None = None):
-        """Numerics mode (``mode`` wins over ``round_bf16``):
+    def __init__(self, cfg, weights: dict, mode: str = "engine"):
+        """Numerics mode:
 
-        * ``"bf16"`` (default) -- the engine's contract (module docstring, DESIGN.md §2);
-        * ``"fp32"`` (``round_bf16=False``) -- every activation rounding off: un-rounded Llama,
+        * ``"engine"`` (default) -- the HIP engine's fp16 contract (module docstring, DESIGN.md
+          §2): weights held as fp16 (exact for bf16-valued weights), the rounding points below
+          with fp16 RNE, and P rounded to fp16 before P.V as the flash kernels do (unnormalised
+          p = exp(s - max) rounded, the row sum taken in fp32 before rounding);
+        * ``"bf16"`` -- the round-3 contract: the same points with bf16 rounding and exact P
+          (kept to show why the engine moved to fp16: tools/parity_modes_cpu.py);
+        * ``"fp32"`` -- every activation rounding off: un-rounded Llama,
           the mode pinned against transformers.LlamaForCausalLM;
         * ``"f16"`` -- ggml's CPU graph for an F16 GGUF, the arithmetic Ollama runs for
           ``llama3.2:3b-instruct-fp16`` (EXT llama.cpp ``llm_build_llama`` without flash
@@ -127,12 +133,12 @@ class OracleLlama:
           to fp16 for V.P, the attention output and SwiGLU product rounded to fp16 at their
           matmuls; fp32 accumulation, fp32 residual, RMSNorm sum of squares in double."""
         self.cfg = cfg
-        self.mode = mode if mode is not None else ("bf16" if round_bf16 else "fp32")
+        self.mode = mode
         assert self.mode in self.MODES, self.mode
-        if self.mode == "f16":
+        if self.mode in ("f16", "engine"):
             weights = _f16_weights(weights)
         self.w = weights
-        self.rnd = {"bf16": bf16_rne, "fp32": _f32, "f16": _f16}[self.mode]
+        self.rnd = {"engine": _f16, "bf16": bf16_rne, "fp32": _f32, "f16": _f16}[self.mode]
 
     def new_cache(self):
         return {"k": [None] * self.cfg.n_layers, "v": [None] * self.cfg.n_layers, "len": 0}
@@ -184,10 +190,15 @@ class OracleLlama:
             s = np.where(mask[None], np.float32(-np.inf), s)
             s = s - s.max(axis=-1, keepdims=True)
             p = np.exp(s)
-            p = p / p.sum(axis=-1, keepdims=True)
-            if f16:  # V.P: ggml rounds the fp32 probabilities to the F16 V's vec_dot type
-                p = _f16(p)
-            o = rnd(np.matmul(p.astype(np.float32), vq.transpose(1, 0, 2)).transpose(1, 0, 2))  # [T, Hq, D]
+            den = p.sum(axis=-1, keepdims=True)
+            if self.mode == "engine":  # flash kernels: fp16(p) . V, then / the fp32 row sum
+                pv = np.matmul(_f16(p), vq.transpose(1, 0, 2)) / den
+            else:
+                p = p / den
+                if f16:  # V.P: ggml rounds the fp32 probabilities to the F16 V's vec_dot type
+                    p = _f16(p)
+                pv = np.matmul(p.astype(np.float32), vq.transpose(1, 0, 2))
+            o = rnd(pv.transpose(1, 0, 2))  # [T, Hq, D]
             x = x + o.reshape(T, Hq * D) @ L["wo"].T
             xg, r = normed(x, L["ffn_norm"])
             g = r * (xg @ L["w_gate"].T)

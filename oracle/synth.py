@@ -97,3 +97,8 @@ def make_weights(cfg, seed: int, std: float = 0.02, jitter: float = 0.0) -> dict
         })
     w["lm_head"] = w["embed"] if cfg.tie_embeddings else linear(seed, LM_HEAD, 0, cfg.vocab, H, std)
     return w
+
+
+def f16_rne(x: np.ndarray) -> np.ndarray:
+    """float32 -> nearest-even IEEE fp16 (the engine's 16-bit type), returned as float32."""
+    return np.asarray(x, dtype=np.float32).astype(np.float16).astype(np.float32)

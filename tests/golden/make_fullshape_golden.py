@@ -7,9 +7,16 @@ weights (oracle/synth.py; all 28 layers, full widths) over BASELINE.json configs
 The call being replaced: run_full_evaluation_pipeline.py:80-106 (one /api/generate per chunk).
 
 Two models (tests/golden/sharp_model.py explains the second):
-  flat  -- the bench weights (seed 77, std 0.02, norm jitter 0.1), chunks 0 and 5;
-  sharp -- the same with a layer-0 RoPE copy head and a shared embedding direction, chunks 0
-           and 3: greedy choices are decisive, so the literal free-running bar applies.
+  flat  -- the bench's exact weights (bench.py: seed 0, std 0.02, norm jitter 0), chunks 0 and 5;
+  sharp -- seed 77 (norm jitter 0.1) with a RoPE copy head at a late layer and a large shared
+           embedding direction, chunks 0 and 3: greedy choices are decisive, so the literal
+           free-running bar applies, and the head reads a residual that all the random layers
+           before it have written.
+
+Three numerics modes of the oracle (oracle/llama_ref.py OracleLlama mode):
+  fp32   -- un-rounded Llama (pinned against transformers on TINY): the parity target;
+  f16    -- ggml's F16 graph, what Ollama runs for the reference's llama3.2:3b-instruct-fp16;
+  engine -- the engine's own fp16 rounding points (a kernel-regression mirror).
 
 Per chunk (key prefix c<k>_):
   prompt      int32 [P]
@@ -24,8 +31,8 @@ Per chunk (key prefix c<k>_):
   gen_top_ids int32 [G][16], gen_top_vals f32 [G][16]: the oracle's top-16 at each step
                                   (step j's context = prompt + gen_ids[:j])
 
-    python tests/golden/make_fullshape_golden.py --which flat
-    python tests/golden/make_fullshape_golden.py --which sharp
+    python tests/golden/make_fullshape_golden.py --which flat --mode fp32   (-> fullshape_flat_fp32.npz)
+    python tests/golden/make_fullshape_golden.py --which sharp --mode engine
 """
 from __future__ import annotations
 
@@ -45,7 +52,7 @@ for p in (ROOT, PKG, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-SEED, STD, JIT = 77, 0.02, 0.1
+MODEL = {"flat": (0, 0.02, 0.0), "sharp": (77, 0.02, 0.1)}  # seed, std, norm jitter
 P, GEN, TOPK = 2048, 128, 16
 SKETCH_SEED = 1234
 CHUNKS = {"flat": (0, 5), "sharp": (0, 3)}
@@ -82,6 +89,7 @@ def topk(v, k=TOPK):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--which", choices=("flat", "sharp"), required=True)
+    ap.add_argument("--mode", choices=("fp32", "f16", "engine"), required=True)
     ap.add_argument("--gen", type=int, default=GEN)
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
@@ -91,8 +99,10 @@ def main():
 
     cfg = LLAMA32_3B
     t0 = time.time()
+    SEED, STD, JIT = MODEL[args.which]
     w = make_weights(cfg, SEED, std=STD, jitter=JIT)
     meta = {"model": cfg.name, "n_layers": cfg.n_layers, "seed": SEED, "std": STD, "jitter": JIT,
+            "mode": args.mode,
             "prompt_len": P, "gen": args.gen, "which": args.which, "chunks_doc": 0,
             "chunks": list(CHUNKS[args.which]), "sketch_seed": SKETCH_SEED,
             "generator": "tests/golden/make_fullshape_golden.py (oracle/llama_ref.py, numpy "
@@ -100,9 +110,10 @@ def main():
     if args.which == "sharp":
         import sharp_model
         w = sharp_model.apply(w, sharp_model.copy_head_overrides(cfg, SEED, JIT))
-        meta.update(copy_offset=sharp_model.COPY_OFFSET, design_seed=sharp_model.DESIGN_SEED)
+        meta.update(copy_offset=sharp_model.COPY_OFFSET, design_seed=sharp_model.DESIGN_SEED,
+                    copy_layer=sharp_model.COPY_LAYER)
     print(f"weights {time.time() - t0:.0f} s", flush=True)
-    o = OracleLlama(cfg, w)
+    o = OracleLlama(cfg, w, mode=args.mode)
     R, Rv = sketch_mats(cfg.hidden, cfg.vocab)
     out = {"meta": np.frombuffer(json.dumps(meta).encode(), np.uint8)}
     for ci, prompt in zip(CHUNKS[args.which], chunks_of(cfg, CHUNKS[args.which])):
@@ -142,7 +153,7 @@ def main():
         gaps = np.stack(gtv)[:, 0] - np.stack(gtv)[:, 1]
         print(f"chunk {ci}: decode {time.time() - t1:.0f} s; top-2 gap min {gaps.min():.4f} "
               f"median {np.median(gaps):.4f}", flush=True)
-    path = args.out or os.path.join(HERE, f"fullshape_{args.which}.npz")
+    path = args.out or os.path.join(HERE, f"fullshape_{args.which}_{args.mode}.npz")
     np.savez_compressed(path, **out)
     print(f"wrote {path} ({os.path.getsize(path) / 1e6:.1f} MB) in {time.time() - t0:.0f} s")
 

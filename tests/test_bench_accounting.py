@@ -17,7 +17,7 @@ def test_prefill_flops_match_survey():
 
 
 def test_decode_weight_bytes_match_survey():
-    # §8d: W = 6,425,149,440 B of bf16 weights per decode step incl. the tied lm_head
+    # §8d: W = 6,425,149,440 B of fp16 weights per decode step incl. the tied lm_head
     cfg, B = LLAMA32_3B, 8
     act = bench.gemv_bytes_per_step(cfg, B) - bench.gemv_bytes_per_step(cfg, 0)
     w = bench.gemv_bytes_per_step(cfg, 0) + cfg.vocab * cfg.hidden * 2

@@ -11,7 +11,7 @@ import pytest
 from mapsum import _lib as L
 from mapsum import gguf
 from mapsum.config import TINY
-from mapsum.weights import f32_to_bf16_bits
+from mapsum.weights import f32_to_f16_bits
 from oracle import quants as Q
 from oracle.synth import make_weights
 
@@ -70,10 +70,10 @@ class Recorder:
     cfg = TINY
 
     def __init__(self):
-        self.bf16, self.q = {}, {}
+        self.f16, self.q = {}, {}
 
     def load_tensor(self, tensor, layer, bits):
-        self.bf16[(tensor, layer)] = np.asarray(bits)
+        self.f16[(tensor, layer)] = np.asarray(bits)
 
     def load_tensor_q(self, tensor, layer, qt, blocks):
         self.q[(tensor, layer)] = (qt, np.asarray(blocks))
@@ -99,11 +99,11 @@ def test_float_gguf_loads_logical_weights(tmp_path):
     assert meta["general.name"] == "tiny-test" and len(ts) == 2 + 9 * TINY.n_layers
     eng = Recorder()
     gguf.load_gguf(eng, path)
-    assert np.array_equal(eng.bf16[(L.MS_T_EMBED, 0)], f32_to_bf16_bits(w["embed"]))
+    assert np.array_equal(eng.f16[(L.MS_T_EMBED, 0)], f32_to_f16_bits(w["embed"]))
     for i, ly in enumerate(w["layers"]):
         for n, t in _T.items():
-            assert np.array_equal(eng.bf16[(t, i)], f32_to_bf16_bits(ly[n])), (i, n)
-        assert np.array_equal(eng.bf16[(L.MS_T_ATTN_NORM, i)], f32_to_bf16_bits(ly["attn_norm"]))
+            assert np.array_equal(eng.f16[(t, i)], f32_to_f16_bits(ly[n])), (i, n)
+        assert np.array_equal(eng.f16[(L.MS_T_ATTN_NORM, i)], f32_to_f16_bits(ly["attn_norm"]))
 
 
 def test_quant_gguf_loads_unpermuted_blocks(tmp_path):

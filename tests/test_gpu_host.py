@@ -168,7 +168,7 @@ def test_failed_chunk_is_isolated_and_requeued(toy):
     embedding row for one of its tokens) finishes MS_FINISH_ERROR on its own; the batch
     companions' summaries are unchanged, and the host re-queues the failed chunk once."""
     from mapsum import _lib as L
-    from mapsum.weights import f32_to_bf16_bits
+    from mapsum.weights import f32_to_f16_bits
     from oracle.synth import make_weights
     cfg = TINY.with_(vocab=toy.tk.get_vocab_size(), bos_id=toy.bos_id, eos_ids=())
     e = Engine(cfg, device=0, max_batch=4, max_ctx=512, max_prefill_tokens=2048)
@@ -180,7 +180,7 @@ def test_failed_chunk_is_isolated_and_requeued(toy):
         before = e.generate(good, 8, ignore_eos=True)
         emb = make_weights(cfg.with_(n_layers=1), 11, std=0.05, jitter=0.1)["embed"].copy()
         emb[333] = np.nan
-        e.load_tensor(L.MS_T_EMBED, 0, f32_to_bf16_bits(emb))
+        e.load_tensor(L.MS_T_EMBED, 0, f32_to_f16_bits(emb))
         res = e.generate(good + [bad], 8, ignore_eos=True, retries=0)
         assert [r.ids for r in res[:3]] == [r.ids for r in before]
         assert res[3].finish == "error" and res[3].ids == []

@@ -14,7 +14,7 @@ torch = pytest.importorskip("torch")
 from mapsum import _lib as L  # noqa: E402
 from mapsum.config import TINY  # noqa: E402
 from mapsum.engine import Engine  # noqa: E402
-from mapsum.weights import f32_to_bf16_bits, load_logical  # noqa: E402
+from mapsum.weights import f32_to_f16_bits, load_logical  # noqa: E402
 from oracle.llama_ref import OracleLlama  # noqa: E402
 from oracle.synth import make_weights  # noqa: E402
 
@@ -58,15 +58,15 @@ def _stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-def _bf16(t):
-    return t.to(torch.bfloat16)
+def _f16(t):
+    return t.to(torch.float16)
 
 
 # ------------------------------------------------------------------ op level
 @pytest.mark.parametrize("M,N,K", [(256, 384, 512), (200, 256, 768), (1, 128, 64), (130, 96, 192),
                                    (512, 1024, 4096), (300, 768, 192), (257, 512, 64), (1000, 1280, 640),
                                    (64, 320, 128)])
-@pytest.mark.parametrize("epi", [L.MS_EPI_STORE_BF16, L.MS_EPI_ADD_F32, L.MS_EPI_STORE_F32, L.MS_EPI_SWIGLU])
+@pytest.mark.parametrize("epi", [L.MS_EPI_STORE_F16, L.MS_EPI_ADD_F32, L.MS_EPI_STORE_F32, L.MS_EPI_SWIGLU])
 @pytest.mark.parametrize("variant", [1, 2])
 def test_gemm_epilogues(lib, dev, M, N, K, epi, variant):
     """Prefill GEMM (128x128 two-stage tile = variant 1, 256x256 8-phase tile = variant 2)
@@ -74,14 +74,14 @@ def test_gemm_epilogues(lib, dev, M, N, K, epi, variant):
     if epi == L.MS_EPI_SWIGLU and N % 32:
         pytest.skip("swiglu needs N % 32 == 0")
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + epi)
-    A = _bf16(torch.randn(M, K, generator=g)).to(dev)
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    A = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
     ref = (A.double().cpu() @ W.double().cpu().T).to(dev)
     if epi == L.MS_EPI_SWIGLU:
-        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros(M, N // 2, dtype=torch.float16, device=dev)
         ldo = N // 2
-    elif epi == L.MS_EPI_STORE_BF16:
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    elif epi == L.MS_EPI_STORE_F16:
+        out = torch.zeros(M, N, dtype=torch.float16, device=dev)
         ldo = N
     else:
         out = torch.randn(M, N, generator=g).to(dev)
@@ -93,7 +93,7 @@ def test_gemm_epilogues(lib, dev, M, N, K, epi, variant):
         torch.cuda.synchronize()
     finally:
         lib.ms_set_gemm_variant(0)
-    if epi == L.MS_EPI_STORE_BF16:
+    if epi == L.MS_EPI_STORE_F16:
         exp, tol = ref, 4e-3
     elif epi == L.MS_EPI_ADD_F32:
         exp, tol = base.double() + ref, 2e-6
@@ -108,20 +108,20 @@ def test_gemm_epilogues(lib, dev, M, N, K, epi, variant):
 
 @pytest.mark.parametrize("M", [1, 3, 8, 16, 17, 40, 64])
 @pytest.mark.parametrize("N,K", [(768, 768), (4096, 768), (768, 2048), (5120, 3072)])
-@pytest.mark.parametrize("epi", [L.MS_EPI_STORE_BF16, L.MS_EPI_ADD_F32, L.MS_EPI_SWIGLU])
+@pytest.mark.parametrize("epi", [L.MS_EPI_STORE_F16, L.MS_EPI_ADD_F32, L.MS_EPI_SWIGLU])
 def test_gemv_vs_torch(lib, dev, M, N, K, epi):
     g = torch.Generator(device="cpu").manual_seed(M * 13 + N + K + epi)
-    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
     ws = torch.zeros(lib.ms_op_gemv_workspace(M, N, K), dtype=torch.uint8, device=dev)
     ref = X.float() @ W.float().T
     if epi == L.MS_EPI_SWIGLU:
-        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros(M, N // 2, dtype=torch.float16, device=dev)
         ldo = N // 2
         r = ref.view(M, N // 32, 2, 16)
         exp = (torch.nn.functional.silu(r[:, :, 0, :]) * r[:, :, 1, :]).reshape(M, N // 2)
-    elif epi == L.MS_EPI_STORE_BF16:
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    elif epi == L.MS_EPI_STORE_F16:
+        out = torch.zeros(M, N, dtype=torch.float16, device=dev)
         ldo = N
         exp = ref
     else:
@@ -141,7 +141,7 @@ def test_gemv_vs_torch(lib, dev, M, N, K, epi):
 
 
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 256])
-@pytest.mark.parametrize("N,K,S,epi", [(1024, 768, 1, L.MS_EPI_STORE_BF16), (768, 2048, 1, L.MS_EPI_ADD_F32),
+@pytest.mark.parametrize("N,K,S,epi", [(1024, 768, 1, L.MS_EPI_STORE_F16), (768, 2048, 1, L.MS_EPI_ADD_F32),
                                        (2048, 768, 1, L.MS_EPI_SWIGLU), (3072, 8192, 4, L.MS_EPI_STORE_F32),
                                        (5120, 3072, 6, L.MS_EPI_STORE_F32), (4096, 768, 1, L.MS_EPI_ARGMAX)])
 def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
@@ -149,8 +149,8 @@ def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
     differ only by summation order; split-K slabs are the exact partial products; the
     argmax partials merge to the fp32 logits' argmax."""
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + S + epi)
-    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
     ref = X.double().cpu() @ W.double().cpu().T
     if epi == L.MS_EPI_STORE_F32:
         out = torch.full((S, M, N), float("nan"), device=dev)
@@ -174,11 +174,11 @@ def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
                 assert int(got[r]) == int(torch.argmax(ref[r])), r
         return
     if epi == L.MS_EPI_SWIGLU:
-        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros(M, N // 2, dtype=torch.float16, device=dev)
         r = ref.view(M, N // 32, 2, 16)
         exp, ldo, tol = (torch.nn.functional.silu(r[:, :, 0]) * r[:, :, 1]).reshape(M, N // 2), N // 2, 4e-3
-    elif epi == L.MS_EPI_STORE_BF16:
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    elif epi == L.MS_EPI_STORE_F16:
+        out = torch.zeros(M, N, dtype=torch.float16, device=dev)
         exp, ldo, tol = ref, N, 4e-3
     else:
         out = torch.randn(M, N, generator=g).to(dev)
@@ -195,8 +195,8 @@ def test_gemv_split_slabs_vs_fp64(lib, dev, M, N, K, S):
     """Split-K decode GEMV: slab s is exactly the partial product over its K range (fp32
     sum order only), and the slabs add up to the full product."""
     g = torch.Generator(device="cpu").manual_seed(M + N + K + S)
-    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
     slabs = torch.full((S, M, N), float("nan"), device=dev)
     L.check(lib.ms_op_gemv_split(X.data_ptr(), W.data_ptr(), slabs.data_ptr(), M, N, K, S, 0, _stream()))
     torch.cuda.synchronize()
@@ -214,13 +214,13 @@ def _ssq_ref(x):
 @pytest.mark.parametrize("S", [0, 1, 4])
 def test_residual_rmsnorm(lib, dev, S):
     """Residual fold + the next normalised projection's input: x += slabs (slab order),
-    y = bf16(x * w), ssq = sum of x^2 -- the deferred RMSNorm."""
+    y = f16(x * w), ssq = sum of x^2 -- the deferred RMSNorm."""
     g = torch.Generator(device="cpu").manual_seed(11 + S)
     rows, H = 8, 3072
     x = (torch.randn(rows, H, generator=g) * 3).to(dev)
     slabs = torch.randn(max(S, 1), rows, H, generator=g).to(dev)
-    w = _bf16(1 + 0.1 * torch.randn(H, generator=g)).to(dev)
-    y = torch.empty(rows, H, dtype=torch.bfloat16, device=dev)
+    w = _f16(1 + 0.1 * torch.randn(H, generator=g)).to(dev)
+    y = torch.empty(rows, H, dtype=torch.float16, device=dev)
     ssq = torch.full((rows,), float("nan"), device=dev)
     xr = x.clone()
     if S:
@@ -233,7 +233,7 @@ def test_residual_rmsnorm(lib, dev, S):
                                        ssq.data_ptr(), rows, H, _stream()))
     torch.cuda.synchronize()
     assert torch.equal(x, xr) if S else torch.equal(x, x0)  # same adds in the same order
-    assert torch.equal(y, (xr * w.float()).to(torch.bfloat16))  # one RNE rounding of x * w
+    assert torch.equal(y, (xr * w.float()).to(torch.float16))  # one RNE rounding of x * w
     assert rel(ssq.double().cpu(), _ssq_ref(xr.cpu())) < 1e-6
     y2 = torch.empty_like(y)
     ssq2 = torch.empty_like(ssq)
@@ -247,28 +247,34 @@ def test_residual_rmsnorm(lib, dev, S):
 @pytest.mark.parametrize("M,rt", [(1, 12), (8, 12), (13, 16)])
 def test_gemv_resid_epilogue(lib, dev, M, rt):
     """Decode O / down with the residual update fused (the engine's small-regime layer): x +=
-    X . W^T, xg = bf16(x * gamma), per-tile sums of the new x^2; a projection scaled from those
+    X . W^T, xg = f16(x * gamma), per-tile sums of the new x^2; a projection scaled from those
     256 partial sums equals rmsnorm(x) * gamma . W^T (the deferred RMSNorm)."""
     g = torch.Generator(device="cpu").manual_seed(M * 100 + rt)
     N, K, eps = 3072, 3072, 1e-5
-    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
-    W = _bf16(torch.randn(N, K, generator=g) * 0.03).to(dev)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.03).to(dev)
     x = (torch.randn(M, N, generator=g) * 2).to(dev)
-    gamma = _bf16(1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    gamma = _f16(1 + 0.1 * torch.randn(N, generator=g)).to(dev)
     x_ref = x.double().cpu() + X.double().cpu() @ W.double().cpu().T
-    xg = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+    xg = torch.empty(M, N, dtype=torch.float16, device=dev)
     tiles = N // rt
     ssq = torch.full((tiles, M), float("nan"), device=dev)
     L.check(lib.ms_op_gemv_resid(X.data_ptr(), W.data_ptr(), x.data_ptr(), xg.data_ptr(), gamma.data_ptr(),
                                  ssq.data_ptr(), M, N, K, rt, _stream()))
     torch.cuda.synchronize()
     assert rel(x.double().cpu(), x_ref) < 1e-6
-    assert torch.equal(xg, (x * gamma.float()).to(torch.bfloat16))  # from the stored x exactly
+    want = (x * gamma.float()).to(torch.float16)  # from the stored x exactly
+    bad = (xg != want).nonzero()
+    if bad.numel():
+        i, j = bad[0].tolist()
+        print(f"xg mismatches {bad.shape[0]} / {xg.numel()}; first ({i}, {j}): x {x[i, j].item()!r} "
+              f"gamma {gamma[i * 0 + j].item()!r} xg {xg[i, j].item()!r} want {want[i, j].item()!r}")
+    assert bad.numel() == 0
     for t in (0, tiles // 2, tiles - 1):
         exp = (x[:, t * rt:(t + 1) * rt].double() ** 2).sum(-1).cpu()
         assert rel(ssq[t].double().cpu(), exp) < 1e-6, t
     # the consumer: QKV-like projection scaled by the 256-tile statistics
-    Wq = _bf16(torch.randn(1024, N, generator=g) * 0.03).to(dev)
+    Wq = _f16(torch.randn(1024, N, generator=g) * 0.03).to(dev)
     out = torch.empty(M, 1024, device=dev)
     ws = torch.zeros(256, dtype=torch.uint8, device=dev)
     L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), tiles, N, eps))
@@ -291,7 +297,7 @@ def test_row_scale_epilogues(lib, dev, path):
     (gate and up both scaled before silu); the argmax epilogue skips it (r > 0 keeps the order)."""
     g = torch.Generator(device="cpu").manual_seed(hash(path) % 1000)
     M, K, eps = 8, 3072, 1e-5
-    X = _bf16(torch.randn(M, K, generator=g)).to(dev)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
     ssq = (torch.rand(M, generator=g) * 5000 + 100).to(dev)
     r = (1.0 / torch.sqrt(ssq.double().cpu() / K + eps))[:, None]
     ws = torch.zeros(256, dtype=torch.uint8, device=dev)
@@ -301,7 +307,7 @@ def test_row_scale_epilogues(lib, dev, path):
             q4 = Q.GGML_TYPE_Q4_K
             N = 512
             blocks = Q.random_blocks(q4, N * K // 256, seed=3)
-            bf = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+            bf = torch.empty(N, K, dtype=torch.float16, device=dev)
             packed = torch.empty(N * (K // 256) * 144, dtype=torch.uint8, device=dev)
             bl = torch.from_numpy(blocks.reshape(-1)).to(dev)
             L.check(lib.ms_op_quant_rows(q4, bl.data_ptr(), N, K, bf.data_ptr(), packed.data_ptr(), _stream()))
@@ -316,7 +322,7 @@ def test_row_scale_epilogues(lib, dev, path):
             assert rel(out.double().cpu(), exp) < 1e-5
             return
         N = 1024
-        W = _bf16(torch.randn(N, K, generator=g) * 0.03).to(dev)
+        W = _f16(torch.randn(N, K, generator=g) * 0.03).to(dev)
         exp = r * (X.double().cpu() @ W.double().cpu().T)
         if path == "gemv_split":
             S = 4
@@ -338,7 +344,7 @@ def test_row_scale_epilogues(lib, dev, path):
         torch.cuda.synchronize()
         assert rel(out.double().cpu(), exp) < 1e-5
         # SwiGLU (rows interleaved gate/up per 16): silu(r g) * (r u)
-        h = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+        h = torch.empty(M, N // 2, dtype=torch.float16, device=dev)
         if path == "gemv":
             L.check(lib.ms_op_gemv(X.data_ptr(), W.data_ptr(), h.data_ptr(), M, N, K, N // 2, L.MS_EPI_SWIGLU,
                                    ws.data_ptr(), _stream()))
@@ -379,8 +385,8 @@ def test_lm_head_argmax_epilogue(lib, dev, M):
     finite logit -> -1 (the engine's per-chunk MS_FINISH_ERROR)."""
     K, N = 768, 4096
     g = torch.Generator(device="cpu").manual_seed(M)
-    X = _bf16(torch.randn(M, K, generator=g))
-    W = _bf16(torch.randn(N, K, generator=g) * 0.05)
+    X = _f16(torch.randn(M, K, generator=g))
+    W = _f16(torch.randn(N, K, generator=g) * 0.05)
     X[0] = 0.0  # row 0: every logit 0 -> a full tie -> id 0
     W[1234] = W[77]  # duplicate rows: exact ties between ids 77 and 1234
     if M > 1:
@@ -414,15 +420,15 @@ def test_lm_head_argmax_epilogue(lib, dev, M):
 def test_rmsnorm_and_argmax(lib, dev):
     g = torch.Generator(device="cpu").manual_seed(5)
     x = (torch.randn(37, 768, generator=g) * 3).to(dev)
-    w = _bf16(1 + 0.1 * torch.randn(768, generator=g)).to(dev)
-    y = torch.empty(37, 768, dtype=torch.bfloat16, device=dev)
+    w = _f16(1 + 0.1 * torch.randn(768, generator=g)).to(dev)
+    y = torch.empty(37, 768, dtype=torch.float16, device=dev)
     ssq = torch.empty(37, device=dev)
     idx = torch.arange(36, -1, -1, dtype=torch.int32, device=dev)  # gathered rows, reversed
     L.check(lib.ms_op_rmsnorm(x.data_ptr(), w.data_ptr(), y.data_ptr(), ssq.data_ptr(), 37, 768, idx.data_ptr(),
                               _stream()))
     torch.cuda.synchronize()
     xs = x.flip(0)
-    assert torch.equal(y, (xs * w.float()).to(torch.bfloat16))
+    assert torch.equal(y, (xs * w.float()).to(torch.float16))
     assert rel(ssq.double().cpu(), _ssq_ref(xs.cpu())) < 1e-6
     lg = torch.randn(5, 128256, generator=g).to(dev)
     lg[2, 77] = 100.0
@@ -704,7 +710,7 @@ def test_dequant_bit_exact_vs_c_oracle(lib, dev, qtype):
 def _decode_weights(qtype, b, wbf):
     """The weights the decode GEMV computes with: Q4_K -- the exact fp32 dequantisation
     (the kernel applies d1 / m1 per sub-block after an MFMA on the integer quants); Q6_K --
-    the bf16 copy (dequantised to bf16 in registers)."""
+    the fp16 copy (dequantised to fp16 in registers)."""
     if qtype == Q.GGML_TYPE_Q4_K:
         return torch.from_numpy(Q.c_dequant(b, qtype).reshape(wbf.shape)).double()
     return wbf.double().cpu()
@@ -713,7 +719,7 @@ def _decode_weights(qtype, b, wbf):
 def _packed(lib, dev, qtype, rows, K, seed):
     b = Q.random_blocks(qtype, rows * K // 256, seed=seed)
     bd = torch.from_numpy(b.reshape(-1)).to(dev)
-    wbf = torch.empty(rows, K, dtype=torch.bfloat16, device=dev)
+    wbf = torch.empty(rows, K, dtype=torch.float16, device=dev)
     pk = torch.empty(rows * (K // 256) * (144 if qtype == Q.GGML_TYPE_Q4_K else 224), dtype=torch.uint8, device=dev)
     L.check(lib.ms_op_quant_rows(qtype, bd.data_ptr(), rows, K, wbf.data_ptr(), pk.data_ptr(), _stream()))
     torch.cuda.synchronize()
@@ -721,33 +727,40 @@ def _packed(lib, dev, qtype, rows, K, seed):
 
 
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
-def test_quant_rows_bf16_copy_is_rounded_dequant(lib, dev, qtype):
+def test_quant_rows_f16_copy_is_rounded_dequant(lib, dev, qtype):
     b, wbf, _ = _packed(lib, dev, qtype, 48, 768, 6)
     want = Q.c_dequant(b, qtype).reshape(48, 768)
-    from oracle.synth import bf16_rne
+    from oracle.synth import f16_rne
     got = wbf.float().cpu().numpy()
-    assert np.array_equal(got, bf16_rne(want))
+    assert np.array_equal(got, f16_rne(want))
+
+
+def _qtol(qtype):
+    """fp32-output tolerance against fp64 on the dequantised weights: Q4_K feeds its codes to the
+    fp16 MFMA as subnormals q * 2^-24 (k_qgemv.hip), where the matrix core keeps ~3e-6 relative
+    (measured 2.9-3.9e-6 over the shapes below) -- 100x below the fp16 rounding of x itself"""
+    return 1e-5 if qtype == Q.GGML_TYPE_Q4_K else 2e-6
 
 
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
 @pytest.mark.parametrize("M", [1, 8, 16, 33])
-@pytest.mark.parametrize("N,K,epi", [(256, 768, L.MS_EPI_STORE_BF16), (512, 2048, L.MS_EPI_ADD_F32),
+@pytest.mark.parametrize("N,K,epi", [(256, 768, L.MS_EPI_STORE_F16), (512, 2048, L.MS_EPI_ADD_F32),
                                      (1024, 768, L.MS_EPI_SWIGLU), (128, 8192, L.MS_EPI_STORE_F32)])
 def test_qgemv_vs_torch(lib, dev, qtype, M, N, K, epi):
     b, wbf, pk = _packed(lib, dev, qtype, N, K, 7 + M)
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
-    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
-    # fp64 reference on the host: fp32 outputs may differ only by summation order, bf16
+    X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
+    # fp64 reference on the host: fp32 outputs may differ only by summation order, fp16
     # outputs additionally by one rounding
     ref = (X.double().cpu() @ _decode_weights(qtype, b, wbf).T).to(dev)
-    tol = 2e-6 if epi in (L.MS_EPI_STORE_F32, L.MS_EPI_ADD_F32) else 4e-3
+    tol = _qtol(qtype) if epi in (L.MS_EPI_STORE_F32, L.MS_EPI_ADD_F32) else 4e-3
     if epi == L.MS_EPI_SWIGLU:
-        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=dev)
+        out = torch.zeros(M, N // 2, dtype=torch.float16, device=dev)
         r = ref.view(M, N // 32, 2, 16)
         exp = (torch.nn.functional.silu(r[:, :, 0, :]) * r[:, :, 1, :]).reshape(M, N // 2)
         ldo = N // 2
-    elif epi == L.MS_EPI_STORE_BF16:
-        out = torch.zeros(M, N, dtype=torch.bfloat16, device=dev)
+    elif epi == L.MS_EPI_STORE_F16:
+        out = torch.zeros(M, N, dtype=torch.float16, device=dev)
         exp, ldo = ref, N
     elif epi == L.MS_EPI_ADD_F32:
         out = torch.randn(M, N, generator=g).to(dev)
@@ -769,7 +782,7 @@ def test_qgemv_argmax_vs_fp64(lib, dev, qtype, M, N, K):
     are within fp32 noise."""
     b, wbf, pk = _packed(lib, dev, qtype, N, K, 5 + M)
     g = torch.Generator(device="cpu").manual_seed(3 * M + N + K)
-    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
     ref = X.double().cpu() @ _decode_weights(qtype, b, wbf).T
     part = torch.full((M, N // 16, 2), float("nan"), device=dev)
     ids = torch.empty(M, dtype=torch.int32, device=dev)
@@ -794,7 +807,7 @@ def test_qgemv_split_slabs_vs_fp64(lib, dev, qtype, M, N, K, S):
     sum order only); the slabs add up to the full product; bad splits are refused."""
     b, wbf, pk = _packed(lib, dev, qtype, N, K, 11 + M + S)
     g = torch.Generator(device="cpu").manual_seed(M + N + K + S)
-    X = torch.randn(M, K, generator=g).to(torch.bfloat16).to(dev)
+    X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
     slabs = torch.full((S, M, N), float("nan"), device=dev)
     L.check(lib.ms_op_qgemv_split(X.data_ptr(), qtype, pk.data_ptr(), slabs.data_ptr(), M, N, K, S,
                                   _stream()))
@@ -802,16 +815,16 @@ def test_qgemv_split_slabs_vs_fp64(lib, dev, qtype, M, N, K, S):
     Xd, Wd, ks = X.double().cpu(), _decode_weights(qtype, b, wbf), K // S
     for s_ in range(S):
         exp = Xd[:, s_ * ks:(s_ + 1) * ks] @ Wd[:, s_ * ks:(s_ + 1) * ks].T
-        assert rel(slabs[s_].double().cpu(), exp) < 2e-6, s_
-    assert rel(slabs.double().sum(0).cpu(), Xd @ Wd.T) < 2e-6
+        assert rel(slabs[s_].double().cpu(), exp) < _qtol(qtype), s_
+    assert rel(slabs.double().sum(0).cpu(), Xd @ Wd.T) < _qtol(qtype)
     assert lib.ms_op_qgemv_split(X.data_ptr(), qtype, pk.data_ptr(), slabs.data_ptr(), M, N, K, 5,
                                  _stream()) != 0
 
 
 def _quant_model(seed):
     """Tiny Q4_K_M-style model: raw blocks per matrix + the oracle's view of it
-    (weights = bf16_rne(dequant(blocks)))."""
-    from oracle.synth import bf16_rne, make_weights
+    (weights = f16_rne(dequant(blocks)))."""
+    from oracle.synth import f16_rne, make_weights
     base = make_weights(TINY, SEED, std=STD, jitter=JITTER)  # norms reused
     H, D, F, V = TINY.hidden, TINY.head_dim, TINY.ffn, TINY.vocab
     shapes = {"wq": (TINY.n_heads * D, H), "wk": (TINY.n_kv_heads * D, H), "wv": (TINY.n_kv_heads * D, H),
@@ -820,7 +833,7 @@ def _quant_model(seed):
     qt = Q.q4_k_m_type("embed", 0, TINY.n_layers)
     eb = Q.random_blocks(qt, V * H // 256, seed=seed, scale=STD)
     qw["embed"] = (qt, eb)
-    w["embed"] = bf16_rne(Q.dequant(eb, qt)).reshape(V, H)
+    w["embed"] = f16_rne(Q.dequant(eb, qt)).reshape(V, H)
     w["lm_head"] = w["embed"]
     for l in range(TINY.n_layers):
         ly = {"attn_norm": base["layers"][l]["attn_norm"], "ffn_norm": base["layers"][l]["ffn_norm"]}
@@ -828,7 +841,7 @@ def _quant_model(seed):
             qt = Q.q4_k_m_type(name, l, TINY.n_layers)
             blk = Q.random_blocks(qt, r * c // 256, seed=seed * 1000 + l * 10 + i, scale=STD)
             qw[(l, name)] = (qt, blk)
-            ly[name] = bf16_rne(Q.dequant(blk, qt)).reshape(r, c)
+            ly[name] = f16_rne(Q.dequant(blk, qt)).reshape(r, c)
         w["layers"].append(ly)
     return qw, w
 
@@ -850,7 +863,7 @@ def _teacher_forced_agreement(oracle, prompt, gen):
 
 def test_quantized_engine_greedy_vs_oracle(dev):
     """Config 5 end to end on the tiny model: K-quant decode GEMVs (fused path, B <= 16)
-    and bf16(dequant) prefill against the oracle run on the same dequantised weights."""
+    and f16(dequant) prefill against the oracle run on the same dequantised weights."""
     from mapsum.weights import load_quantized
     qw, w = _quant_model(3)
     # the 2-layer tiny model uses the Q4_K_M mix: both types occur

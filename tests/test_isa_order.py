@@ -80,7 +80,7 @@ def test_gemv_x_dma_precedes_weight_stream(tmp_path):
             wl = [k for k in range(first) if ops[k].startswith("global_load") and not ops[k].startswith("global_load_lds")]
             assert dma and wl, name
             # loads above the last DMA may only be the residual epilogue's x / gamma prefetch
-            # (gemv_common.h resid_prefetch: one dword, one bf16)
+            # (gemv_common.h resid_prefetch: one dword, one fp16)
             pre = [ops[k] for k in wl if k < max(dma)]
             assert len(pre) <= 2 and all(o in ("global_load_dword", "global_load_ushort") for o in pre), \
                 f"{name}: a weight load was scheduled above the X DMA ({pre})"

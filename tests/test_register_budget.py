@@ -1,7 +1,7 @@
 """Register-budget guard for the decode GEMVs whose speed depends on occupancy (CPU: reads the
 built library's code-object metadata).
 
-The gate/up GEMV of the bf16 decode step (k_gemv.hip gemv_kernel<1, 2, SWIGLU, 3, kXLds, RS>)
+The gate/up GEMV of the fp16 decode step (k_gemv.hip gemv_kernel<1, 2, SWIGLU, 3, kXLds, RS>)
 runs 1024-thread blocks and streams its weights with two blocks co-resident per CU, which
 needs <= 64 VGPRs per lane (2 x 16 waves over 4 SIMDs x 512 VGPRs).  One extra live register
 -- a row statistic held across the weight stream -- took it to 67 and cost 1.6 us per launch

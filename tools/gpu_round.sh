@@ -7,7 +7,7 @@
 #   usage: bash tools/gpu_round.sh [bench args...]   (e.g. --weights q4_k_m)
 export TMPDIR=/tmp; mkdir -p gpurun_out
 O=gpurun_out; R=/tmp/msprof; rm -rf $R; mkdir -p $R
-TAG=${TAG:-bf16}
+TAG=${TAG:-f16}
 if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -3 $O/gpu_tests.log

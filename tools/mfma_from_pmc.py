@@ -6,7 +6,7 @@ usage: mfma_from_pmc.py <counter_collection.csv> <out.json> [kernel substrings..
 
 Per dispatch, rows of one counter are summed (rocprofv3 may split a counter over
 instances).  MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts matrix-pipe cycles
-(16 per v_mfma_f32_16x16x32_bf16 = 16,384 FLOP, i.e. 1,024 FLOP per busy cycle) summed over
+(16 per v_mfma_f32_16x16x32_f16 (or _bf16) = 16,384 FLOP, i.e. 1,024 FLOP per busy cycle) summed over
 every SIMD; GRBM_GUI_ACTIVE is the busy clock summed over the 8 XCDs.  So
     util = MFMA_BUSY / (GRBM_GUI_ACTIVE / 8 * 1024 SIMDs)
 is the fraction of the chip's matrix-pipe cycles the kernel kept busy while it ran,

@@ -26,4 +26,4 @@ for line in r.stderr.splitlines():
 for name, d in rows.items():
     if pat in name:
         print(f"{d.get('VGPRs', '?'):>4} {d.get('AGPRs', '?'):>4} occ={d.get('Occupancy [waves/SIMD]', '?'):>2} "
-              f"lds={d.get('LDS Size [bytes/block]', '?'):>6}  {name}")
+              f"lds={d.get('LDS Size [bytes/block]', '?'):>6} scratch={d.get('ScratchSize [bytes/lane]', '?'):>3}  {name}")
