@@ -204,6 +204,13 @@ int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t*
 /* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0 */
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* stream);
+/* prefill O / down with the residual update fused (the engine's prefill layer): x fp32 [M][N] +=
+   A . W^T, and the input of the next normalised projection: xg_out fp16 [M][N] = f16(x * gamma),
+   ssq_out fp32 [tiles][M] = per-column-tile sums of the new x^2 (tiles = ms_gemm_resid_tiles(M, N)),
+   the deferred RMSNorm statistics the next ms_op_gemm takes through ms_op_set_row_scale */
+int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const void* gamma, float* ssq_out,
+                     int32_t M, int32_t N, int32_t K, void* stream);
+int ms_gemm_resid_tiles(int32_t M, int32_t N);
 /* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase) */
 int ms_set_gemm_variant(int32_t variant);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */

@@ -139,12 +139,16 @@ struct ms_engine {
   // launches, the K-quant and large-regime form: the K-quant GEMV with this epilogue on 12-row
   // tiles measured no faster than split-K 4 + residual_rmsnorm, 1.962 vs 1.955 ms per Q4_K_M
   // decode step, profiles/r03/v7_q4_resid_fused_rejected.txt).
-  bool resid_fuse = true, has_quant = false, warned_quant_large = false;
+  bool resid_fuse = true, has_quant = false;
   int resid_rt = 12;
   bool resid_fused(const QSlot* q) const {
     return resid_fuse && !large_engine && !(q && q->ready());
   }
-  bool large(int) const { return large_engine; }
+  // the large-batch arithmetic (skinny GEMM on the fp16 weights) for engines of >= dgemm_min
+  // slots -- except engines with K-quant weights: they keep the exact Q4_K / Q6_K GEMV at every
+  // batch size, in row groups of <= kMaxGemvRows (a row's sum order does not depend on its group)
+  bool large(int) const { return large_engine && !has_quant; }
+  bool row_groups(int B) const { return !large(B) && B > kMaxGemvRows; }
   // split count of every quantised slab projection (MS_QSPLIT; 0: as fp16): 4 measured best
   // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the fp16 splits (6 / 6 / 4), 2 / 3 / 8
   // slower (profiles/r02/v27_qsplit_sweep_q4_k_m.txt)
@@ -288,9 +292,19 @@ struct ms_engine {
     prof_end(cls);
   }
 
-  // decode projection: the K-quant stream when that matrix was loaded quantised
+  // decode projection: the K-quant stream when that matrix was loaded quantised; above
+  // kMaxGemvRows rows (row groups) the rows go in groups, out elements of `esz` bytes
   void proj(const QSlot* q, const f16_t* X, const f16_t* W, void* out, int M, int N, int K,
-            int ldo, int epi, const GemvArgs* ga, int cls) {
+            int ldo, int epi, const GemvArgs* ga, int cls, int esz = 0) {
+    if (row_groups(M)) {
+      for (int r0 = 0; r0 < M; r0 += kMaxGemvRows) {
+        GemvArgs g = ga ? *ga : GemvArgs{};
+        g.rs = rs_rows(g.rs, r0);
+        proj(q, X + (size_t)r0 * K, W, (char*)out + (size_t)r0 * ldo * esz, std::min(M - r0, (int)kMaxGemvRows),
+             N, K, ldo, epi, &g, cls, esz);
+      }
+      return;
+    }
     prof_begin(cls);
     if (q && q->ready() && qgemv_supported(M, N, K, epi))
       launch_qgemv(X, q->m, out, M, N, K, ldo, epi, ga, stream);
@@ -311,12 +325,23 @@ struct ms_engine {
              dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32) &&
              dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU) && (2 * F) % 32 == 0 &&
              attn_decode_supported(B, Hq, Hk, max_pages * kPage);
-    return B <= kMaxGemvRows && residual_rmsnorm_supported(kMaxSplit, H) &&
-           (attn_slabs ? gemv_split_supported(B, QKVN, H, 1) : gemv_supported(B, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(B, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
-           gemv_split_supported(B, H, Hq * D, 1) && gemv_split_supported(B, H, F, 1) &&
-           (!resid_fuse || (gemv_supported(B, H, Hq * D, MS_GEMV_EPI_RESID_SSQ) &&
-                            gemv_supported(B, H, F, MS_GEMV_EPI_RESID_SSQ))) &&
+    // row groups (K-quant engines above 64 rows): split-K slabs and SwiGLU only, no residual
+    // epilogue (resid_fused is off in large engines), one residual_rmsnorm over all rows
+    if (row_groups(B) && !(B <= kMaxSlabRows && attn_slabs && !resid_fused(nullptr))) return false;
+    const int Bg = std::min(B, (int)kMaxGemvRows);
+    return residual_rmsnorm_supported(kMaxSplit, H) &&
+           (attn_slabs ? gemv_split_supported(Bg, QKVN, H, 1) : gemv_supported(Bg, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(Bg, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
+           gemv_split_supported(Bg, H, Hq * D, 1) && gemv_split_supported(Bg, H, F, 1) &&
+           (!resid_fuse || (gemv_supported(Bg, H, Hq * D, MS_GEMV_EPI_RESID_SSQ) &&
+                            gemv_supported(Bg, H, F, MS_GEMV_EPI_RESID_SSQ))) &&
            attn_decode_supported(B, Hq, Hk, max_pages * kPage);
+  }
+  // a row group's deferred-norm scale: one-tile statistics are per row ([M]), so the group
+  // starts at its first row (multi-tile [tiles][M] statistics never reach row groups)
+  static RowScale rs_rows(const RowScale& rs, int r0) {
+    RowScale g = rs;
+    if (g.ssq) g.ssq += r0;
+    return g;
   }
   static constexpr int kMaxGemvRows = 64, kMaxSlabRows = 256, kMaxSplit = 8;
 
@@ -324,9 +349,23 @@ struct ms_engine {
   // the number of slabs written
   int proj_split(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
                  const RowScale* rs) {
+    if (row_groups(M)) {
+      int used = 1;
+      for (int r0 = 0; r0 < M; r0 += kMaxGemvRows) {
+        const RowScale g = rs ? rs_rows(*rs, r0) : RowScale{};
+        used = proj_split_rows(q, X + (size_t)r0 * K, W, std::min(M - r0, (int)kMaxGemvRows), N, K, S, Sl,
+                               rs ? &g : nullptr, slabs + (size_t)r0 * N, M);
+      }
+      return used;
+    }
+    return proj_split_rows(q, X, W, M, N, K, S, Sl, rs, slabs, 0);
+  }
+  int proj_split_rows(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
+                      const RowScale* rs, float* slabs, int slab_rows) {
     prof_begin(K_GEMV);
     GemvArgs ga{};
     if (rs) ga.rs = *rs;
+    ga.slab_rows = slab_rows;
     int used = 1;
     if (large(M)) {  // skinny GEMM on the fp16 weights (K-quant copies included)
       launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
@@ -421,7 +460,7 @@ struct ms_engine {
     } else {
       GemvArgs gg{};
       gg.rs = rs_ffn;
-      proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV);
+      proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV, sizeof(f16_t));
     }
     const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
     resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next);
@@ -439,11 +478,18 @@ struct ms_engine {
     const Layer& Ly = layers[l];
     const int kc = decode ? K_GEMV : K_GEMM;
     const RowScale rs_attn = cur_rs;
-    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
     KVView kv = kv_layer(l);
-    prof_begin(K_MISC);
-    launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
-    prof_end(K_MISC);
+    if (decode) {
+      gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
+      prof_begin(K_MISC);
+      launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
+      prof_end(K_MISC);
+    } else {  // prefill: RoPE and the K / V scatter in the QKV GEMM's epilogue
+      const GemmRope gp{tok_pos, tok_slot, cos_tab, sin_tab, kv, Hq, Hk};
+      prof_begin(K_GEMM);
+      launch_gemm(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, kGemmEpiRopeKV, stream, &rs_attn, nullptr, &gp);
+      prof_end(K_GEMM);
+    }
     if (decode) {
       prof_begin(K_ATTN_DECODE);
       launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}}, attn, Hq, Hk, kv, da, attn_ws, stream);
@@ -453,12 +499,34 @@ struct ms_engine {
       launch_attn_prefill(qkv, attn, Hq, Hk, kv, pa, stream);
       prof_end(K_ATTN_PREFILL);
     }
-    gemm_or_gemv(attn, Ly.wo, x, T, H, Hq * D, H, MS_EPI_ADD_F32, decode, kc);
-    norm_input(Ly.ffn_norm, T);
+    const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
+    if (decode) {
+      gemm_or_gemv(attn, Ly.wo, x, T, H, Hq * D, H, MS_EPI_ADD_F32, decode, kc);
+      norm_input(Ly.ffn_norm, T);
+    } else {  // prefill: the O GEMM's residual epilogue emits the gate/up input and statistics
+      prefill_resid(attn, Ly.wo, T, Hq * D, Ly.ffn_norm);
+    }
     const RowScale rs_ffn = cur_rs;
     gemm_or_gemv(xb, Ly.wgu, hbuf, T, 2 * F, H, F, MS_EPI_SWIGLU, decode, kc, &rs_ffn);
-    gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
-    if (tail) norm_input(l + 1 < L ? layers[l + 1].attn_norm : final_norm, T);
+    if (decode) {
+      gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
+      if (tail) norm_input(g_next, T);
+    } else if (tail) {
+      prefill_resid(hbuf, Ly.wdown, T, F, g_next);
+    } else {
+      gemm_or_gemv(hbuf, Ly.wdown, x, T, H, F, H, MS_EPI_ADD_F32, decode, kc);
+    }
+  }
+
+  // prefill residual update x += X . W^T whose GEMM epilogue also writes xb = f16(x * g_next)
+  // and per-column-tile sums of x^2 (k_gemm.hip GemmResid): no norm launch between the
+  // residual add and the next normalised projection
+  void prefill_resid(const f16_t* X, const f16_t* W, int T, int K, const f16_t* g_next) {
+    GemmResid gr{g_next, xb, ssq};
+    prof_begin(K_GEMM);
+    launch_gemm(X, W, x, T, H, K, H, MS_EPI_ADD_F32, stream, nullptr, &gr);
+    prof_end(K_GEMM);
+    cur_rs = make_row_scale(ssq, gemm_resid_tiles(T, H), H, cfg.norm_eps);
   }
 
   // xb = f16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
@@ -661,7 +729,8 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {  // prefill: T rows; decode: max_batch rows
       const size_t R = c == &E.cp ? T : (size_t)cfg->max_batch;
       c->x = E.dalloc<float>(R * E.H);
-      c->ssq = E.dalloc<float>(std::max(R, (size_t)256 * cfg->max_batch), true);
+      // [rows] (norm kernels), [256][rows] (decode RESID epilogue), [tiles][rows] (prefill GEMM)
+      c->ssq = E.dalloc<float>(std::max(R * kGemmRsTiles, (size_t)256 * cfg->max_batch), true);
       c->xb = E.dalloc<f16_t>(R * E.H);
       c->qkv = E.dalloc<f16_t>(R * E.QKVN);
       c->attn = E.dalloc<f16_t>(R * E.Hq * E.D);
@@ -1234,10 +1303,12 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     E.prof_begin(K_MISC);
     launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
     E.prof_end(K_MISC);
-  } else if (gemv_supported(B, E.V, E.H, MS_GEMV_EPI_ARGMAX)) {
+  } else if (gemv_supported(std::min(B, (int)ms_engine::kMaxGemvRows), E.V, E.H, MS_GEMV_EPI_ARGMAX) &&
+             (B <= ms_engine::kMaxGemvRows || E.row_groups(B))) {
     // greedy argmax in the lm_head epilogue: {max, id} per 16-column tile, no logits row
     const int tiles = E.V / 16;
-    E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, nullptr, K_LMHEAD);
+    E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, nullptr, K_LMHEAD,
+           sizeof(float2));
     E.prof_begin(K_MISC);
     launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
     E.prof_end(K_MISC);
@@ -1364,13 +1435,6 @@ int ms_step(ms_engine* e) {
     // of k chained steps (one host synchronisation), k bounded by the nearest num_predict, the
     // attention split grid and kMaxRun; k = 1 while admissible work waits for a free slot
     E.use(E.cd);
-    if (E.large_engine && E.has_quant && !E.warned_quant_large) {
-      // say so instead of silently changing arithmetic with the engine size
-      fprintf(stderr, "libmapsum: a %d-slot engine decodes in the large-batch regime: K-quant matrices are "
-              "multiplied from their fp16 dequantised copies (skinny MFMA GEMM); the exact fp32 K-quant GEMV "
-              "runs in engines of < %d slots\n", E.cfg.max_batch, E.dgemm_min);
-      E.warned_quant_large = true;
-    }
     std::vector<Seq*> batch;
     for (auto& s : E.running)
       if (!s->finish && s->len > 0) batch.push_back(s.get());
@@ -1568,10 +1632,23 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
   return op_guard([&] {
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
-    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "gemm row scale: one-tile statistics only");
+    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles <= kGemmRsTiles, MS_EINVAL, "gemm row scale: at most 24 tiles of statistics");
     launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }
+
+int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const void* gamma, float* ssq_out,
+                     int32_t M, int32_t N, int32_t K, void* stream) {
+  return op_guard([&] {
+    REQUIRE(A && W && x && xg_out && gamma && ssq_out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL,
+            "bad gemm_resid operands (K % 64 == 0)");
+    REQUIRE(gemm_resid_tiles(M, N) <= kGemmRsTiles, MS_EINVAL, "gemm_resid: N over 24 column tiles");
+    GemmResid gr{(const f16_t*)gamma, (f16_t*)xg_out, ssq_out};
+    launch_gemm((const f16_t*)A, (const f16_t*)W, x, M, N, K, N, MS_EPI_ADD_F32, (hipStream_t)stream, nullptr, &gr);
+  });
+}
+
+int ms_gemm_resid_tiles(int32_t M, int32_t N) { return gemm_resid_tiles(M, N); }
 
 int ms_set_gemm_variant(int32_t v) {
   if (v < 0 || v > 2) return MS_EINVAL;

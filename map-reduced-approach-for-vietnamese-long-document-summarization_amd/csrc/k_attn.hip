@@ -72,7 +72,7 @@ __device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x
 // barrier per tile.  The swizzles are applied on the DMA source (lane i of a 1-KiB piece lands
 // at chunk i % 16 of row i / 16, so it loads the global chunk that belongs there); rows past
 // the sequence load the last valid row instead (finite values under P = 0: never NaN * 0 in P.V).
-template <int GB>
+template <int GB, bool STAG>
 __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __restrict__ qkv,
                                                               f16_t* __restrict__ out, int Hq,
                                                               int Hk, KVView kv, PrefillAttnArgs a,
@@ -123,36 +123,32 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   const int ntiles = (kv_end + 63) / 64;
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
 
-  // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
-  // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
-  auto dma_tile = [&](int t, int buf) {
+  // DMA of the K (isv = 0) or V half of tile t into buffer t & 1: this wave's 2 pieces J = 2*wave +
+  // i cover rows 4J .. 4J+3; lane -> row 4J + lane / 16, LDS chunk lane % 16
+  auto dma_half = [&](int t, int isv) {
     const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];
     const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
     const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
-    char* img = smem + buf * 32768;
+    char* img = smem + (t & 1) * 32768 + isv * 16384;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int J = 4 * wave + i, isv = J >> 4;
-      const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
+    for (int i = 0; i < 2; ++i) {
+      const int J = 2 * wave + i;
+      const int row = 4 * J + (lane >> 4), c = lane & 15;
       const int srow = min(row, lim - 1);
       const int sch = isv ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
       const f16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (LDS_AS void*)(img + isv * 16384 + 4 * (J & 15) * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(img + 4 * J * 256), 16, 0, 0);
     }
   };
-  dma_tile(0, 0);
-  for (int t = 0; t < ntiles; ++t) {
-    // tile t landed (its DMA is the only global load in flight), and every wave is past
-    // tile t-1, whose buffer the next DMA overwrites
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + 1 < ntiles) dma_tile(t + 1, (t + 1) & 1);
-    if (!wave_live || t * 64 > wave_qlast) continue;  // wave-uniform: keys after every query
+  f32x4 sc[GB][4];  // the scores of one tile, from the wave's QK phase to its softmax / PV phase
+  // phase A: S^T = K . Q^T of tile t for the GB heads (each K fragment feeds GB MFMAs)
+  auto phase_a = [&](int t) {
     const char* ks_ = smem + (t & 1) * 32768;
-    const char* vs_ = ks_ + 16384;
-
-    f32x4 sc[GB][4];
+    // the Q image offset laundered per tile: hoisted out of the tile loop, the GB x 4 Q fragments
+    // (48 VGPRs) stayed live across it and pushed the kernel into scratch
+    int qo = (int)(qimg - smem);
+    asm volatile("" : "+v"(qo));
+    const char* qi_ = smem + qo;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -162,9 +158,13 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
         const f16x8 kf = *(const f16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh)
-          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
+          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qi_ + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
       }
     }
+  };
+  // phase B: mask, online softmax and O^T += V^T . P^T of tile t
+  auto phase_b = [&](int t) {
+    const char* vs_ = smem + (t & 1) * 32768 + 16384;
     // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
     // first query or the sequence end can hold any
     const bool masked = (t * 64 + 63 > wave_qpos0) || (t * 64 + 64 > kvlen);
@@ -231,6 +231,49 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
       }
+  };
+  auto live = [&](int t) { return wave_live && t >= 0 && t < ntiles && t * 64 <= wave_qlast; };
+
+  dma_half(0, 0);
+  dma_half(0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // tile 0 and the Q image
+  if constexpr (STAG) {
+    // Two wave groups one phase apart: slot 2t runs group 0's phase A of tile t beside group 1's
+    // phase B of tile t-1, slot 2t+1 group 0's B(t) beside group 1's A(t).  Waves w and w+4 share
+    // a SIMD, so every SIMD has one wave on QK MFMAs while the other runs its softmax (VALU) and
+    // PV; in lockstep both waves of a SIMD sat in the same phase.  K(t+1) is issued at slot 2t
+    // (K(t-1)'s last reader, group 1's A(t-1), ended with slot 2t-1) and V(t+1) at slot 2t+1
+    // (V(t-1) last read in slot 2t): each half has two slots to land.  A slot ends with this
+    // wave's DMA of that slot still in flight (vmcnt(2): the older half landed) and a barrier.
+    const bool g1 = wave >= 4;
+    for (int k = 0; k <= 2 * ntiles; ++k) {
+      const int tn = (k >> 1) + 1;  // the tile whose K (k even) or V (k odd) is issued now
+      const bool issue = tn < ntiles;
+      if (issue) dma_half(tn, k & 1);
+      const bool pa = ((k & 1) == 0) != g1;
+      const int t = pa ? (k >> 1) : (g1 ? (k >> 1) - 1 : (k >> 1));
+      if (live(t)) {
+        if (pa) phase_a(t);
+        else phase_b(t);
+      }
+      if (issue) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) {
+      if (t + 1 < ntiles) {  // every wave is past tile t-1, whose buffer this overwrites
+        dma_half(t + 1, 0);
+        dma_half(t + 1, 1);
+      }
+      if (live(t)) {
+        phase_a(t);
+        phase_b(t);
+      }
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // tile t+1 landed
+      __builtin_amdgcn_s_barrier();
+    }
   }
   if (wave_live && qi < qlen) {
 #pragma unroll
@@ -248,6 +291,11 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   }
 }
 
+static bool prefill_stagger() {
+  static const bool v = [] { const char* e = getenv("MS_ATTN_STAGGER"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s) {
   if (a.n_qblk <= 0) return;
@@ -255,10 +303,11 @@ void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv
   const int G = Hq / Hk;
   const int gb = (G % 3 == 0) ? 3 : (G % 2 == 0) ? 2 : 1;
   const dim3 grid(a.n_qblk * (Hq / gb));
-#define AP(GB_) MS_LAUNCH(attn_prefill_kernel<GB_>, grid, dim3(512), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
-  if (gb == 3) AP(3);
-  else if (gb == 2) AP(2);
-  else AP(1);
+  const bool st = prefill_stagger();
+#define AP(GB_, ST_) MS_LAUNCH((attn_prefill_kernel<GB_, ST_>), grid, dim3(512), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
+  if (gb == 3) { if (st) AP(3, true); else AP(3, false); }
+  else if (gb == 2) { if (st) AP(2, true); else AP(2, false); }
+  else { if (st) AP(1, true); else AP(1, false); }
 #undef AP
 }
 

@@ -18,6 +18,8 @@
 // per 16 on upload) so no extra HBM pass is spent on them; the normalised projections (QKV,
 // gate/up, logits) scale each output row by its deferred RMSNorm factor (kernels.h RowScale,
 // one tile: rs_rinv(ssq[row])).
+#include <type_traits>
+
 #include "kernels.h"
 
 namespace ms {
@@ -31,15 +33,133 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 
 __device__ __forceinline__ float silu_mul(float g, float u) { return g / (1.0f + __expf(-g)) * u; }
 
+// ---- deferred-norm statistics of the consumers (epilogues 0, 2, 3).  One tile: the rows' sums
+// of squares by LDS DMA straight into rinv_s; more (a residual epilogue's per-column-tile
+// partials, [tiles][M]): staged, then folded in tile order into rinv_s before the epilogue.
+// Issued ahead of the first K tile (no register: a register load here made the compiler drain
+// vmcnt inside the K loop).
+template <int BM, int NW>
+__device__ __forceinline__ void gemm_rs_dma(const RowScale& rs, int M, int m0, float* rinv_s, float* stage) {
+  if (!rs.ssq) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (rs.tiles == 1) {
+    if (wave < BM / 64)
+      __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(m0 + wave * 64 + lane, M - 1)),
+                                       (LDS_AS void*)(rinv_s + wave * 64), 4, 0, 0);
+    return;
+  }
+  for (int p = wave; p < rs.tiles * (BM / 64); p += NW) {
+    const int t = p / (BM / 64), r0 = (p % (BM / 64)) * 64;
+    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + (size_t)t * M + min(m0 + r0 + lane, M - 1)),
+                                     (LDS_AS void*)(stage + t * BM + r0), 4, 0, 0);
+  }
+}
+template <int BM>
+__device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, const float* stage) {
+  if (!rs.ssq || rs.tiles == 1) return;  // block-uniform
+  __syncthreads();  // every wave is past its K loop (the DMA landed before the first tile)
+  if ((int)threadIdx.x < BM) {
+    float sum = 0.f;
+    for (int t = 0; t < rs.tiles; ++t) sum += stage[t * BM + threadIdx.x];
+    rinv_s[threadIdx.x] = sum;
+  }
+  __syncthreads();
+}
+// ---- epilogue 4 (prefill QKV): RoPE + K / V scatter.  The output columns of a 16-column group
+// are one tile of a rope-permuted Q / K head (lane fr < 8 holds dim 8t + fr, lane fr + 8 its
+// rotate-half partner 64 + 8t + fr) or 16 dims of a V head.  Per row: its position and cache row
+// once; per element: the fp16-rounded value (rope_kv_kernel's input), the partner by a lane
+// shuffle, rope_kv_kernel's rotation, the store.  Unrolled at compile time (Unroll<>): with
+// runtime loop indices the compiler kept the 128 accumulators of the 256x256 tile in scratch.
+template <int I, int N>
+struct Unroll {
+  template <class F>
+  __device__ __forceinline__ static void run(F&& f) {
+    f(std::integral_constant<int, I>{});
+    Unroll<I + 1, N>::run(f);
+  }
+};
+template <int N>
+struct Unroll<N, N> {
+  template <class F>
+  __device__ __forceinline__ static void run(F&&) {}
+};
+struct RopeRow {
+  int pos;
+  bool valid;
+  size_t kv_off;  // element offset of (page, kv head 0, pos % 64, dim 0) in the cache
+};
+__device__ __forceinline__ RopeRow rope_row(const GemmRope& gp, int row, int M) {
+  RopeRow r;
+  const int rr = min(row, M - 1);
+  r.valid = row < M;
+  r.pos = gp.pos[rr];
+  const KVView& kv = gp.kv;
+  const int page = kv.block_table[(size_t)gp.slot[rr] * kv.max_pages + r.pos / kPage];
+  r.kv_off = ((size_t)page * kv.n_kv_heads * kPage + r.pos % kPage) * kHeadDim;
+  return r;
+}
+__device__ __forceinline__ void gemm_rope_store(const GemmRope& gp, f16_t* qkv, int ldo, int row, const RopeRow& rw,
+                                                int col0, int fr, float a, int N) {
+  const float v = h2f(f2h(a));  // q / k / v rounded to fp16 first: rope_kv_kernel's input
+  const float pv = __shfl_xor(v, 8, 64);
+  const int QD = gp.Hq * kHeadDim, KD = gp.Hk * kHeadDim;
+  if (col0 < QD + KD) {  // wave-uniform
+    const int i = 8 * ((col0 & 127) >> 4) + (fr & 7);
+    const bool lo_lane = fr < 8;
+    const float lo = lo_lane ? v : pv, hi = lo_lane ? pv : v;
+    const float cs = gp.cos_tab[(size_t)rw.pos * 64 + i], sn = gp.sin_tab[(size_t)rw.pos * 64 + i];
+    const float o = lo_lane ? __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn))
+                            : __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
+    const int dim = lo_lane ? i : 64 + i;
+    if (!rw.valid || col0 >= N) return;
+    if (col0 < QD) qkv[(size_t)row * ldo + (col0 & ~127) + dim] = f2h(o);
+    else gp.kv.k[rw.kv_off + (size_t)((col0 - QD) >> 7) * kPage * kHeadDim + dim] = f2h(o);
+  } else {
+    if (!rw.valid || col0 >= N) return;
+    gp.kv.v[rw.kv_off + (size_t)((col0 - QD - KD) >> 7) * kPage * kHeadDim + (col0 & 127) + fr] = f2h(v);
+  }
+}
+
+// ---- the residual epilogue's outputs for the next normalised projection
+__device__ __forceinline__ void gemm_resid_xg(const GemmResid& gr, size_t o, float v, float g, float& ss) {
+  float p = v * g;
+  asm volatile("" : "+v"(p));  // the fp32 product, then one fp16 rounding (no v_fma_mixlo_f16)
+  gr.xg[o] = f2h(p);
+  ss += v * v;
+}
+// per-row sums of x^2 over the block's BN columns: lane partials (its NI columns, in order) ->
+// LDS [row][wave column][lane column] -> one thread per row adds them in order.  The tile
+// buffers are free: every wave is past its K loop.
+template <int BM, int WCOLS, int MI>
+__device__ __forceinline__ void gemm_resid_ssq(char* smem, const float (&ss)[MI][4], int wrow0, int wcol,
+                                               int fg, int fr, int M, int m0, int tile, const GemmResid& gr) {
+  float* red = (float*)smem;
+  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[((wrow0 + mi * 16 + fg * 4 + j) * WCOLS + wcol) * 16 + fr] = ss[mi][j];
+  __syncthreads();
+  if ((int)threadIdx.x < BM && m0 + (int)threadIdx.x < M) {
+    const float* p = red + threadIdx.x * WCOLS * 16;
+    float sum = 0.f;
+    for (int q = 0; q < WCOLS * 16; ++q) sum += p[q];
+    gr.ssq[(size_t)tile * M + m0 + threadIdx.x] = sum;
+  }
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ A,
                                                      const f16_t* __restrict__ W,
                                                      void* __restrict__ out, int M, int N, int K,
-                                                     int ldo, RowScale rs) {
-  // 64 KiB of tiles + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
-  // object: with the DMA into a second array the compiler drained vmcnt before every LDS read
-  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GBM * GBK * 2 + GBM * 4];
+                                                     int ldo, RowScale rs, GemmResid gr, GemmRope gp) {
+  // 64 KiB of tiles + the tile rows' sums of squares (deferred-norm statistics: the folded sum,
+  // then up to kGemmRsTiles staged partials).  ONE LDS object: with the DMA into a second array
+  // the compiler drained vmcnt before every LDS read
+  __shared__ __attribute__((aligned(16))) char smem[2 * 2 * GBM * GBK * 2 + GBM * 4 * (1 + kGemmRsTiles)];
   float* rinv_s = (float*)(smem + 2 * 2 * GBM * GBK * 2);
+  float* rs_stage = rinv_s + GBM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + GBM - 1) / GBM, tiles_n = (N + GBN - 1) / GBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
@@ -82,9 +202,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
   const int nk = K / GBK;
   // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
-  if (rs.ssq && wave < GBM / 64)
-    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(m0 + wave * 64 + lane, M - 1)),
-                                     (LDS_AS void*)(rinv_s + wave * 64), 4, 0, 0);
+  gemm_rs_dma<GBM, 4>(rs, M, m0, rinv_s, rs_stage);
   stage(0, 0);
   wait_vmcnt0();
   __syncthreads();
@@ -119,6 +237,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 
   // epilogue: acc[m][n][j] = C[row 4*fg + j][col fr] of 16x16 tile (m, n)
   if constexpr (EPI == 1) {  // residual add: 32 loads in flight, then the adds and stores
+    const bool fuse = gr.xg != nullptr;
+    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+    float ss[4][4] = {};
+    if (fuse)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) g4[n] = h2f(gr.gamma[min(n0 + wn * 64 + n * 16 + fr, N - 1)]);
 #pragma unroll
     for (int m0_ = 0; m0_ < 4; m0_ += 2) {
       float r[2][4][4];
@@ -141,11 +265,17 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
           for (int n = 0; n < 4; ++n) {
             const int row = m0 + wm * 64 + (m0_ + h) * 16 + fg * 4 + j;
             const int col = n0 + wn * 64 + n * 16 + fr;
-            if (row < M && col < N) ((float*)out)[(size_t)row * ldo + col] = r[h][j][n] + acc[m0_ + h][n][j];
+            const float v = r[h][j][n] + acc[m0_ + h][n][j];
+            if (row < M && col < N) {
+              ((float*)out)[(size_t)row * ldo + col] = v;
+              if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, g4[n], ss[m0_ + h][j]);
+            }
           }
     }
+    if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, m0, n0 / GBN, gr);
     return;
   }
+  gemm_rs_fold<GBM>(rs, rinv_s, rs_stage);
   f32x4 rv4[4];  // the rows' norm factors, as gemm256_kernel's epilogue
 #pragma unroll
   for (int m = 0; m < 4; ++m) rv4[m] = f32x4{1.f, 1.f, 1.f, 1.f};
@@ -156,6 +286,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) rv4[m][j] = rs_rinv(rv4[m][j], rs);
+  }
+  if constexpr (EPI == kGemmEpiRopeKV) {
+    Unroll<0, 4>::run([&](auto m) {
+      Unroll<0, 4>::run([&](auto j) {
+        const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
+        const RopeRow rw = rope_row(gp, row, M);
+        Unroll<0, 4>::run([&](auto n) {
+          gemm_rope_store(gp, (f16_t*)out, ldo, row, rw, n0 + wn * 64 + n * 16, fr, acc[m][n][(int)j] * rv4[m][(int)j], N);
+        });
+      });
+    });
+    return;
   }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -218,11 +360,13 @@ template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict__ A,
                                                         const f16_t* __restrict__ W,
                                                         void* __restrict__ out, int M, int N, int K,
-                                                        int ldo, RowScale rs) {
-  // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics).  ONE LDS
-  // object: with the DMA into a second array the compiler drained vmcnt before every LDS read
-  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4];
+                                                        int ldo, RowScale rs, GemmResid gr, GemmRope gp) {
+  // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics: the folded
+  // sum, then up to kGemmRsTiles staged partials).  ONE LDS object: with the DMA into a second
+  // array the compiler drained vmcnt before every LDS read
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemmRsTiles)];
   float* rinv_s = (float*)(smem + 2 * 65536);
+  float* rs_stage = rinv_s + TBM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (N + TBN - 1) / TBN;
   const int pid = xcd_remap(blockIdx.x, gridDim.x);
@@ -308,9 +452,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   const int nk = K / TBK;
   // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
-  if (rs.ssq && wave < TBM / 64)
-    __builtin_amdgcn_global_load_lds((const void*)(rs.ssq + min(m0 + wave * 64 + lane, M - 1)),
-                                     (LDS_AS void*)(rinv_s + wave * 64), 4, 0, 0);
+  gemm_rs_dma<TBM, 8>(rs, M, m0, rinv_s, rs_stage);
   // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
   stage(0, 0, 0);
   stage(0, 3, 0);
@@ -359,7 +501,13 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   if constexpr (EPI == 1) {
     // residual add: the 32 fp32 loads of two 16-row groups are issued together before their
     // adds and stores (a plain `out[o] += acc` compiled to 128 dependent load -> wait ->
-    // store round trips per lane)
+    // store round trips per lane); with gr.xg also the next projection's input and statistics
+    const bool fuse = gr.xg != nullptr;
+    float g4[4] = {0.f, 0.f, 0.f, 0.f};
+    float ss[8][4] = {};
+    if (fuse)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) g4[ni] = h2f(gr.gamma[min(n0 + wc * 64 + ni * 16 + fr, N - 1)]);
 #pragma unroll
     for (int mi0 = 0; mi0 < 8; mi0 += 2) {
       float r[2][4][4];
@@ -385,11 +533,17 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
           for (int ni = 0; ni < 4; ++ni) {
             const int row = m0 + wr * 128 + (mi0 + h) * 16 + fg * 4 + j;
             const int col = n0 + wc * 64 + ni * 16 + fr;
-            if (row < M && col < N) ((float*)out)[(size_t)row * ldo + col] = r[h][j][ni] + acc[mi0 + h][ni][j];
+            const float v = r[h][j][ni] + acc[mi0 + h][ni][j];
+            if (row < M && col < N) {
+              ((float*)out)[(size_t)row * ldo + col] = v;
+              if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, g4[ni], ss[mi0 + h][j]);
+            }
           }
     }
+    if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, m0, n0 / TBN, gr);
     return;
   }
+  gemm_rs_fold<TBM>(rs, rinv_s, rs_stage);
   // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
   // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
   // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
@@ -403,6 +557,18 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
+  }
+  if constexpr (EPI == kGemmEpiRopeKV) {
+    Unroll<0, 8>::run([&](auto mi) {
+      Unroll<0, 4>::run([&](auto j) {
+        const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
+        const RopeRow rw = rope_row(gp, row, M);
+        Unroll<0, 4>::run([&](auto ni) {
+          gemm_rope_store(gp, (f16_t*)out, ldo, row, rw, n0 + wc * 64 + ni * 16, fr, acc[mi][ni][(int)j] * rv4[mi][(int)j], N);
+        });
+      });
+    });
+    return;
   }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
@@ -438,32 +604,48 @@ static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning 
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
+static bool gemm_big(int M, int N) {
+  return g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
+}
+
+int gemm_resid_tiles(int M, int N) { return gemm_big(M, N) ? (N + TBN - 1) / TBN : (N + GBN - 1) / GBN; }
+
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
-                 hipStream_t s, const RowScale* rs_in) {
+                 hipStream_t s, const RowScale* rs_in, const GemmResid* gr_in, const GemmRope* gp_in) {
   if (M <= 0) return;
   RowScale rs{};
   if (rs_in && rs_in->ssq && epi != 1) {
-    if (rs_in->tiles != 1) return;  // callers pass one-tile statistics (a norm kernel's)
+    if (rs_in->tiles < 1 || rs_in->tiles > kGemmRsTiles) return;  // callers check (ms_op_gemm)
     rs = *rs_in;
   }
-  const bool big = g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
-  if (big) {
+  GemmResid gr{};
+  if (gr_in && epi == 1) gr = *gr_in;
+  GemmRope gp{};
+  if (epi == kGemmEpiRopeKV) {
+    if (!gp_in || N % 16) return;  // callers pass the token positions and the cache
+    gp = *gp_in;
+  }
+#define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr, gp)
+  if (gemm_big(M, N)) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {
-      case 0: MS_LAUNCH(gemm256_kernel<0>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
-      case 1: MS_LAUNCH(gemm256_kernel<1>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
-      case 2: MS_LAUNCH(gemm256_kernel<2>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
-      default: MS_LAUNCH(gemm256_kernel<3>, dim3(grid), dim3(512), 0, s, A, W, out, M, N, K, ldo, rs); break;
+      case 0: GL(gemm256_kernel, 0, 512); break;
+      case 1: GL(gemm256_kernel, 1, 512); break;
+      case 2: GL(gemm256_kernel, 2, 512); break;
+      case kGemmEpiRopeKV: GL(gemm256_kernel, kGemmEpiRopeKV, 512); break;
+      default: GL(gemm256_kernel, 3, 512); break;
     }
     return;
   }
   const int grid = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
   switch (epi) {
-    case 0: MS_LAUNCH(gemm_kernel<0>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
-    case 1: MS_LAUNCH(gemm_kernel<1>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
-    case 2: MS_LAUNCH(gemm_kernel<2>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
-    default: MS_LAUNCH(gemm_kernel<3>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, rs); break;
+    case 0: GL(gemm_kernel, 0, 256); break;
+    case 1: GL(gemm_kernel, 1, 256); break;
+    case 2: GL(gemm_kernel, 2, 256); break;
+    case kGemmEpiRopeKV: GL(gemm_kernel, kGemmEpiRopeKV, 256); break;
+    default: GL(gemm_kernel, 3, 256); break;
   }
+#undef GL
 }
 
 }  // namespace ms

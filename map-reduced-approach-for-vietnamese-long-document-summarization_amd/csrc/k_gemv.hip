@@ -97,7 +97,7 @@ __global__ __launch_bounds__(1024) void gemv_kernel(const f16_t* __restrict__ X,
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
     X += (size_t)blockIdx.y * K;
     W += (size_t)blockIdx.y * K;
-    out = (float*)out + (size_t)blockIdx.y * M * ldo;
+    out = (float*)out + (size_t)blockIdx.y * (ga.slab_rows > 0 ? ga.slab_rows : M) * ldo;
   }
 
   // 0. the output rows' deferred-norm partial sums, 1. X (LDS DMA of the block's rows or this

@@ -198,7 +198,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
   const int ldx = K * gridDim.y, sbk = blockIdx.y * (K / 256);
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) {
     X += (size_t)blockIdx.y * K;
-    out = (float*)out + (size_t)blockIdx.y * M * ldo;
+    out = (float*)out + (size_t)blockIdx.y * (ga.slab_rows > 0 ? ga.slab_rows : M) * ldo;
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;

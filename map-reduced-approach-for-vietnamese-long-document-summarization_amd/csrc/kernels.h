@@ -78,10 +78,34 @@ void launch_rope_kv(f16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     KVView kv, hipStream_t s);
 void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s);
 
-// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 fp16, K % 64 == 0; rs (one tile, or null):
-// the deferred RMSNorm scale of the output rows (epilogues 0, 2, 3)
+// out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 fp16, K % 64 == 0; rs (<= kGemmRsTiles tiles of
+// statistics, or null): the deferred RMSNorm scale of the output rows (epilogues 0, 2, 3).
+// gr (epilogue 1, the residual add of O / down): the GEMM also writes the next normalised
+// projection's input, gr->xg = f16(x_new * gr->gamma) [M][N], and per-tile sums of x_new^2,
+// gr->ssq [N / tile][M] (tile = the kernel's column tile; gemm_resid_tiles) -- no norm launch.
+struct GemmResid {
+  const f16_t* gamma;
+  f16_t* xg;
+  float* ssq;
+};
+constexpr int kGemmRsTiles = 24;
+// epilogue 4 (prefill QKV, weight rows rope-permuted as for the decode GEMV): q / k / v rounded to
+// fp16, RoPE on the Q / K heads (rope_kv_kernel's arithmetic), Q stored in natural order into the
+// output rows, K / V scattered into the paged cache -- no rope_kv launch
+constexpr int kGemmEpiRopeKV = 4;
+struct GemmRope {
+  const int32_t* pos;   // [M] token positions
+  const int32_t* slot;  // [M] block-table rows
+  const float* cos_tab;
+  const float* sin_tab;
+  KVView kv;
+  int Hq, Hk;
+};
+// statistics tiles the residual epilogue writes for an M x N GEMM (its column-tile count)
+int gemm_resid_tiles(int M, int N);
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo,
-                 int epi, hipStream_t s, const RowScale* rs = nullptr);
+                 int epi, hipStream_t s, const RowScale* rs = nullptr, const GemmResid* gr = nullptr,
+                 const GemmRope* gp = nullptr);
 // tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
 void set_gemm_variant(int v);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
@@ -120,6 +144,9 @@ struct GemvArgs {
   // deferred RMSNorm scale of the output rows (STORE_F16 / STORE_F32 / SWIGLU / ROPE_KV /
   // ARGMAX epilogues)
   RowScale rs;
+  // split-K slabs: rows between consecutive slabs (0 = M).  A row group of a larger batch
+  // writes its rows into the batch's [S][B][N] slabs (slab_rows = B, out = slab 0, row r0)
+  int slab_rows;
 };
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)

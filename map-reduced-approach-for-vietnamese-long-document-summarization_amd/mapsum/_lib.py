@@ -34,7 +34,7 @@ EXPORTED = (
     "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant",
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
-    "ms_op_gemv_resid", "ms_op_set_row_scale",
+    "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
 )
 
 
@@ -104,6 +104,8 @@ def load() -> C.CDLL:
         "ms_op_gemv_strided": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_resid": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, i32, vp]),
         "ms_op_set_row_scale": (i32, [vp, i32, i32, C.c_float]),
+        "ms_op_gemm_resid": (i32, [vp, vp, vp, vp, vp, vp, i32, i32, i32, vp]),
+        "ms_gemm_resid_tiles": (i32, [i32, i32]),
         "ms_submit_forced": (i32, [vp, pi32, i32, pi32, i32, i32, u32, u64]),
         "ms_op_gemm": (i32, [vp, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_gemv_workspace": (i64, [i32, i32, i32]),

@@ -326,18 +326,22 @@ def q4km(dev):
     return qw, w, OracleLlama(CFG, w)
 
 
+_Q4_GEN = {}
+
+
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("slots", [2, 32])
+@pytest.mark.parametrize("slots", [2, 32, 128])
 def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
     """configs[4] at the full widths (2 layers): Q4_K_M blocks through ms_load_weight_q;
     prefill logits and 64 teacher-forced greedy tokens against the oracle run on the
-    dequantised weights.  slots = 2: the dequant-fused K-quant GEMVs; slots = 32: the
-    large-batch regime, which multiplies the fp16 dequantised copies (tested, and
-    the engine says so on stderr)."""
+    dequantised weights.  Every engine size decodes with the dequant-fused K-quant GEMVs
+    (exact Q4_K arithmetic): 2 slots in one row group, 32 and 128 slots (the large-batch regime
+    of fp16 engines) in row groups of <= 64 -- with 96 chunks in flight at 128 slots the batch
+    really spans two groups -- so the chunk's tokens are the same at every engine size."""
     from mapsum.weights import load_quantized
     qw, w, o = q4km
     prompt = _chunks()[2][:768]
-    e = Engine(CFG, device=0, max_batch=slots, max_ctx=1024, max_prefill_tokens=2048)
+    e = Engine(CFG, device=0, max_batch=slots, max_ctx=1024, max_prefill_tokens=2048 if slots < 128 else 8192)
     try:
         load_quantized(e, qw, w)
         _, lg = e.forward(prompt, hidden=False, logits=True)
@@ -346,7 +350,15 @@ def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
         err = rel(lg, ref_lg)
         noise = float(np.sqrt(np.mean((lg - ref_lg) ** 2)))
         assert err < 2e-2, err
-        gen = np.asarray(e.generate([prompt], num_predict=64, ignore_eos=True)[0].ids)
+        if slots == 128:  # the chunk among 95 others (two row groups of the decode GEMVs)
+            others = [c[:256] for c in _chunks()[3:8]] * 19
+            res = e.generate([prompt] + others, num_predict=64, ignore_eos=True)
+            gen = np.asarray(res[0].ids)
+        else:
+            gen = np.asarray(e.generate([prompt], num_predict=64, ignore_eos=True)[0].ids)
+        _Q4_GEN[slots] = gen
+        if 2 in _Q4_GEN:  # engine-size invariance: the K-quant arithmetic is per row
+            assert np.array_equal(gen, _Q4_GEN[2]), (slots, np.nonzero(gen != _Q4_GEN[2])[0][:5])
         tl = _teacher_forced(o, cache, ref_lg[-1], gen)
         want = np.argmax(tl, 1)
         srt = np.sort(tl, 1)

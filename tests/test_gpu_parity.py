@@ -290,6 +290,52 @@ def test_gemv_resid_epilogue(lib, dev, M, rt):
     assert rel(out.double().cpu(), exp) < 1e-5
 
 
+@pytest.mark.parametrize("M,variant", [(300, 1), (1100, 2), (2048, 0)])
+def test_gemm_resid_epilogue(lib, dev, M, variant):
+    """Prefill O / down with the residual update fused: x += A . W^T, xg = f16(x * gamma) from the
+    stored x exactly, per-column-tile sums of the new x^2 ([tiles][M]); a GEMM scaled from those
+    multi-tile statistics equals rmsnorm(x) * gamma . W^T (the deferred RMSNorm), on both tiles."""
+    g = torch.Generator(device="cpu").manual_seed(M + variant)
+    N, K, eps = 3072, 1024, 1e-5
+    A = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.03).to(dev)
+    x = (torch.randn(M, N, generator=g) * 2).to(dev)
+    gamma = _f16(1 + 0.1 * torch.randn(N, generator=g)).to(dev)
+    x_ref = x.double().cpu() + A.double().cpu() @ W.double().cpu().T
+    xg = torch.empty(M, N, dtype=torch.float16, device=dev)
+    L.check(lib.ms_set_gemm_variant(variant))
+    try:
+        tiles = lib.ms_gemm_resid_tiles(M, N)
+        assert tiles == (12 if (variant == 2 or (variant == 0 and M >= 1024)) else 24)
+        ssq = torch.full((tiles, M), float("nan"), device=dev)
+        L.check(lib.ms_op_gemm_resid(A.data_ptr(), W.data_ptr(), x.data_ptr(), xg.data_ptr(), gamma.data_ptr(),
+                                     ssq.data_ptr(), M, N, K, _stream()))
+        torch.cuda.synchronize()
+        assert rel(x.double().cpu(), x_ref) < 1e-6
+        want = (x * gamma.float()).to(torch.float16)
+        assert int((xg != want).sum()) == 0
+        tw = N // tiles
+        for t in (0, tiles // 2, tiles - 1):
+            exp = (x[:, t * tw:(t + 1) * tw].double() ** 2).sum(-1).cpu()
+            assert rel(ssq[t].double().cpu(), exp) < 1e-6, t
+        # the consumer: a QKV-like GEMM scaled by the multi-tile statistics
+        Wq = _f16(torch.randn(1024, N, generator=g) * 0.03).to(dev)
+        out = torch.empty(M, 1024, device=dev)
+        L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), tiles, N, eps))
+        try:
+            L.check(lib.ms_op_gemm(xg.data_ptr(), Wq.data_ptr(), out.data_ptr(), M, 1024, N, 1024,
+                                   L.MS_EPI_STORE_F32, _stream()))
+        finally:
+            L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
+        torch.cuda.synchronize()
+    finally:
+        L.check(lib.ms_set_gemm_variant(0))
+    xd = x.double().cpu()
+    r = 1.0 / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
+    exp = r * (xg.double().cpu() @ Wq.double().cpu().T)
+    assert rel(out.double().cpu(), exp) < 1e-5
+
+
 @pytest.mark.parametrize("path", ["gemv", "gemv_split", "dgemm", "gemm", "qgemv"])
 def test_row_scale_epilogues(lib, dev, path):
     """Every normalised-projection epilogue applies the deferred RMSNorm factor of its rows:
