@@ -84,7 +84,12 @@ typedef struct ms_config {
   int32_t tie_embeddings;
   /* engine */
   int32_t device;               /* HIP device ordinal                         */
-  int32_t max_batch;            /* sequences in flight (<= 1024)              */
+  int32_t max_batch;            /* sequences in flight (<= 1024).  Also fixes the
+                                   engine's decode arithmetic (fp16 weights):
+                                   1-16 residual-fused GEMV, 17-23 split GEMV +
+                                   residual_rmsnorm, >= 24 skinny GEMM; results
+                                   are batch-invariant inside one engine, not
+                                   across these boundaries */
   int32_t max_ctx;              /* prompt + generated tokens per sequence     */
   int32_t max_prefill_tokens;   /* packed prompt tokens per prefill pass      */
   int32_t n_pages;              /* KV pages of 64 tokens; 0 = enough for all  */

@@ -479,17 +479,13 @@ struct ms_engine {
     const int kc = decode ? K_GEMV : K_GEMM;
     const RowScale rs_attn = cur_rs;
     KVView kv = kv_layer(l);
-    if (decode) {
-      gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
-      prof_begin(K_MISC);
-      launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
-      prof_end(K_MISC);
-    } else {  // prefill: RoPE and the K / V scatter in the QKV GEMM's epilogue
-      const GemmRope gp{tok_pos, tok_slot, cos_tab, sin_tab, kv, Hq, Hk};
-      prof_begin(K_GEMM);
-      launch_gemm(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, kGemmEpiRopeKV, stream, &rs_attn, nullptr, &gp);
-      prof_end(K_GEMM);
-    }
+    // (RoPE + the K / V scatter in the prefill QKV GEMM's epilogue measured slower than this
+    // launch: 611 vs 423 + 58 us per layer, scattered 2-byte stores and per-element table loads,
+    // profiles/r04/v5_prefill_fusions_prof_*.txt)
+    gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
+    prof_begin(K_MISC);
+    launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
+    prof_end(K_MISC);
     if (decode) {
       prof_begin(K_ATTN_DECODE);
       launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}}, attn, Hq, Hk, kv, da, attn_ws, stream);
@@ -526,7 +522,10 @@ struct ms_engine {
     prof_begin(K_GEMM);
     launch_gemm(X, W, x, T, H, K, H, MS_EPI_ADD_F32, stream, nullptr, &gr);
     prof_end(K_GEMM);
-    cur_rs = make_row_scale(ssq, gemm_resid_tiles(T, H), H, cfg.norm_eps);
+    const int tiles = gemm_resid_tiles(T, H);
+    REQUIRE(gemm_rs_tiles_ok(T, QKVN, tiles) && gemm_rs_tiles_ok(T, 2 * F, tiles), MS_EINVAL,
+            "prefill residual statistics: consumer GEMM cannot fold them");
+    cur_rs = make_row_scale(ssq, tiles, H, cfg.norm_eps);
   }
 
   // xb = f16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
@@ -1632,7 +1631,8 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
   return op_guard([&] {
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
-    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles <= kGemmRsTiles, MS_EINVAL, "gemm row scale: at most 24 tiles of statistics");
+    REQUIRE(!g_op_rs.ssq || gemm_rs_tiles_ok(M, N, g_op_rs.tiles), MS_EINVAL,
+            "gemm row scale: at most 24 tiles of statistics (12 for the 256x256 kernel)");
     launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }

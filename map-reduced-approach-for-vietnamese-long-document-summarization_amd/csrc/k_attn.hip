@@ -11,7 +11,7 @@
 //   O^T += V^T . P^T  (A = V^T via ds_read_b64_tr_b16 from a row-major V tile,
 //                      B = P^T taken straight from the S^T accumulators)
 // so the query index sits on the MFMA column (lane & 15) in S^T, P^T and O^T alike:
-// the online-softmax max/sum need only two lane-xor shuffles and the O rescale is
+// the online-softmax max/sum need only two lane-group swaps and the O rescale is
 // lane-local.  The k order inside a PV step is permuted (keys 4g..4g+3 and
 // 16+4g..16+4g+3 for lane group g), identically on both operands.
 // LDS images: K rows swizzled chunk ^ (row & 15) (ds_read_b128, conflict-free);
@@ -51,6 +51,23 @@ __device__ __forceinline__ f16x8 pack_p(const f32x4& a, const f32x4& b) {
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// max / sum over the 4 lane groups of an MFMA column (lanes l, l^16, l^32, l^48) by
+// v_permlane16_swap / v_permlane32_swap: two VALU swaps where __shfl_xor compiled to
+// ds_bpermute LDS round trips on the softmax's critical path.  Same pairing and order as the
+// xor-16-then-xor-32 shuffles (a + b is commutative), so the same bits.
+__device__ __forceinline__ float grp_max(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+__device__ __forceinline__ float grp_sum(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
+}
 // decode KV pages (plain loads: non-temporal ones measured slower, 2.45 vs 2.29 ms per decode
 // step, profiles/r01 v5_nt_stream_ab_rejected)
 __device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x4*)p; }
@@ -65,14 +82,14 @@ __device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x
 // MFMAs -- the round-3 kernel (4 waves x 16 rows, hi + lo bf16 P) held 240 VGPRs + 148 AGPRs at
 // one wave per SIMD and could not hide its own QK -> softmax -> PV chain.  The online softmax
 // works on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)) with a lazily moved reference
-// max (below); the O rescale is skipped when no query column of the wave moved it; the causal /
+// max (below), so the O rescale factor is exactly 1 on most tiles; the causal /
 // sequence-end mask is applied only on tiles that can cross it, and a wave skips the tiles that
 // lie wholly after its last query.  K/V tiles reach LDS by DMA (global_load_lds, no register
 // staging and no ds_write), two buffers: tile t+1 is in flight while tile t is multiplied, one
 // barrier per tile.  The swizzles are applied on the DMA source (lane i of a 1-KiB piece lands
 // at chunk i % 16 of row i / 16, so it loads the global chunk that belongs there); rows past
 // the sequence load the last valid row instead (finite values under P = 0: never NaN * 0 in P.V).
-template <int GB, bool STAG>
+template <int GB>
 __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __restrict__ qkv,
                                                               f16_t* __restrict__ out, int Hq,
                                                               int Hk, KVView kv, PrefillAttnArgs a,
@@ -123,32 +140,40 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   const int ntiles = (kv_end + 63) / 64;
   const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
 
-  // DMA of the K (isv = 0) or V half of tile t into buffer t & 1: this wave's 2 pieces J = 2*wave +
-  // i cover rows 4J .. 4J+3; lane -> row 4J + lane / 16, LDS chunk lane % 16
-  auto dma_half = [&](int t, int isv) {
+  // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
+  // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
+  auto dma_tile = [&](int t, int buf) {
     const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];
     const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
     const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
-    char* img = smem + (t & 1) * 32768 + isv * 16384;
+    char* img = smem + buf * 32768;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int J = 2 * wave + i;
-      const int row = 4 * J + (lane >> 4), c = lane & 15;
+    for (int i = 0; i < 4; ++i) {
+      const int J = 4 * wave + i, isv = J >> 4;
+      const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
       const int srow = min(row, lim - 1);
       const int sch = isv ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
       const f16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src, (LDS_AS void*)(img + 4 * J * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (LDS_AS void*)(img + isv * 16384 + 4 * (J & 15) * 256), 16, 0, 0);
     }
   };
-  f32x4 sc[GB][4];  // the scores of one tile, from the wave's QK phase to its softmax / PV phase
-  // phase A: S^T = K . Q^T of tile t for the GB heads (each K fragment feeds GB MFMAs)
-  auto phase_a = [&](int t) {
+  // Lockstep: every wave runs QK, softmax and PV of tile t between two barriers.  A staggered
+  // schedule (wave groups w < 4 and w >= 4, which share SIMDs, one phase apart so one wave's
+  // QK MFMAs run beside the other's softmax) measured slower: 356 vs 295 us per layer at
+  // configs[1] (two barriers and half-tile DMA waits per tile; profiles/r04/v5_*).
+  dma_tile(0, 0);
+  for (int t = 0; t < ntiles; ++t) {
+    // tile t landed (its DMA is the only global load in flight), and every wave is past
+    // tile t-1, whose buffer the next DMA overwrites
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 1 < ntiles) dma_tile(t + 1, (t + 1) & 1);
+    if (!wave_live || t * 64 > wave_qlast) continue;  // wave-uniform: keys after every query
     const char* ks_ = smem + (t & 1) * 32768;
-    // the Q image offset laundered per tile: hoisted out of the tile loop, the GB x 4 Q fragments
-    // (48 VGPRs) stayed live across it and pushed the kernel into scratch
-    int qo = (int)(qimg - smem);
-    asm volatile("" : "+v"(qo));
-    const char* qi_ = smem + qo;
+    const char* vs_ = ks_ + 16384;
+
+    f32x4 sc[GB][4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt) {
 #pragma unroll
@@ -158,13 +183,9 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
         const f16x8 kf = *(const f16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh)
-          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qi_ + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
+          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
       }
     }
-  };
-  // phase B: mask, online softmax and O^T += V^T . P^T of tile t
-  auto phase_b = [&](int t) {
-    const char* vs_ = smem + (t & 1) * 32768 + 16384;
     // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
     // first query or the sequence end can hold any
     const bool masked = (t * 64 + 63 > wave_qpos0) || (t * 64 + 64 > kvlen);
@@ -180,7 +201,6 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
         }
     }
     f16x8 pf[GB][2];
-    bool rescale = false;
     float alpha[GB];
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh) {
@@ -189,8 +209,7 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int j = 0; j < 4; ++j) mx = fmaxf(mx, sc[hh][mt][j]);
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = grp_max(mx);
       // lazy rescale: the running max only moves when a tile's max exceeds it by more than
       // 8 in log2 units (p <= 2^8 is harmless in fp32 and in fp16 P), so after the first
       // tiles the O accumulators are rarely rescaled; O / l is unchanged by the choice of
@@ -199,7 +218,6 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       const bool grow = m_new != m_run[hh] && !((m_new - m_run[hh]) * scale_log2 <= 8.f);
       const float m_use = grow ? m_new : m_run[hh];
       alpha[hh] = grow ? __builtin_amdgcn_exp2f((m_run[hh] - m_new) * scale_log2) : 1.f;
-      rescale |= grow;
       const float mc = (m_use == -INFINITY) ? 0.f : m_use * scale_log2;
       float rs = 0.f;
 #pragma unroll
@@ -210,19 +228,18 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
           sc[hh][mt][j] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = grp_sum(rs);
       l_run[hh] = l_run[hh] * alpha[hh] + rs;
       m_run[hh] = m_use;
       pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
     }
-    if (__ballot(rescale) != 0) {
+    // unconditional (alpha = 1 exactly unless the reference max moved): a branch here split
+    // the tile into basic blocks the scheduler could not interleave MFMA and VALU across
 #pragma unroll
-      for (int hh = 0; hh < GB; ++hh)
+    for (int hh = 0; hh < GB; ++hh)
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt) o[hh][dt] *= alpha[hh];
-    }
+      for (int dt = 0; dt < 8; ++dt) o[hh][dt] *= alpha[hh];
 #pragma unroll
     for (int kstep = 0; kstep < 2; ++kstep)
 #pragma unroll
@@ -231,49 +248,6 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
       }
-  };
-  auto live = [&](int t) { return wave_live && t >= 0 && t < ntiles && t * 64 <= wave_qlast; };
-
-  dma_half(0, 0);
-  dma_half(0, 1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // tile 0 and the Q image
-  if constexpr (STAG) {
-    // Two wave groups one phase apart: slot 2t runs group 0's phase A of tile t beside group 1's
-    // phase B of tile t-1, slot 2t+1 group 0's B(t) beside group 1's A(t).  Waves w and w+4 share
-    // a SIMD, so every SIMD has one wave on QK MFMAs while the other runs its softmax (VALU) and
-    // PV; in lockstep both waves of a SIMD sat in the same phase.  K(t+1) is issued at slot 2t
-    // (K(t-1)'s last reader, group 1's A(t-1), ended with slot 2t-1) and V(t+1) at slot 2t+1
-    // (V(t-1) last read in slot 2t): each half has two slots to land.  A slot ends with this
-    // wave's DMA of that slot still in flight (vmcnt(2): the older half landed) and a barrier.
-    const bool g1 = wave >= 4;
-    for (int k = 0; k <= 2 * ntiles; ++k) {
-      const int tn = (k >> 1) + 1;  // the tile whose K (k even) or V (k odd) is issued now
-      const bool issue = tn < ntiles;
-      if (issue) dma_half(tn, k & 1);
-      const bool pa = ((k & 1) == 0) != g1;
-      const int t = pa ? (k >> 1) : (g1 ? (k >> 1) - 1 : (k >> 1));
-      if (live(t)) {
-        if (pa) phase_a(t);
-        else phase_b(t);
-      }
-      if (issue) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-    for (int t = 0; t < ntiles; ++t) {
-      if (t + 1 < ntiles) {  // every wave is past tile t-1, whose buffer this overwrites
-        dma_half(t + 1, 0);
-        dma_half(t + 1, 1);
-      }
-      if (live(t)) {
-        phase_a(t);
-        phase_b(t);
-      }
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // tile t+1 landed
-      __builtin_amdgcn_s_barrier();
-    }
   }
   if (wave_live && qi < qlen) {
 #pragma unroll
@@ -291,11 +265,6 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   }
 }
 
-static bool prefill_stagger() {
-  static const bool v = [] { const char* e = getenv("MS_ATTN_STAGGER"); return !e || atoi(e) != 0; }();
-  return v;
-}
-
 void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv,
                          PrefillAttnArgs a, hipStream_t s) {
   if (a.n_qblk <= 0) return;
@@ -303,11 +272,10 @@ void launch_attn_prefill(const f16_t* qkv, f16_t* out, int Hq, int Hk, KVView kv
   const int G = Hq / Hk;
   const int gb = (G % 3 == 0) ? 3 : (G % 2 == 0) ? 2 : 1;
   const dim3 grid(a.n_qblk * (Hq / gb));
-  const bool st = prefill_stagger();
-#define AP(GB_, ST_) MS_LAUNCH((attn_prefill_kernel<GB_, ST_>), grid, dim3(512), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
-  if (gb == 3) { if (st) AP(3, true); else AP(3, false); }
-  else if (gb == 2) { if (st) AP(2, true); else AP(2, false); }
-  else { if (st) AP(1, true); else AP(1, false); }
+#define AP(GB_) MS_LAUNCH(attn_prefill_kernel<GB_>, grid, dim3(512), 0, s, qkv, out, Hq, Hk, kv, a, scale_log2)
+  if (gb == 3) AP(3);
+  else if (gb == 2) AP(2);
+  else AP(1);
 #undef AP
 }
 
@@ -549,8 +517,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
           sc[mt][j] = v;
           mx = fmaxf(mx, v);
         }
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      mx = grp_max(mx);
       const float m_new = fmaxf(m_run, mx);  // finite: key pg*64 < len is always visible
       const float alpha = (m_run == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_run - m_new);
       float rs = 0.f;
@@ -562,8 +529,7 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
           sc[mt][j] = p;
           rs += p;
         }
-      rs += __shfl_xor(rs, 16, 64);
-      rs += __shfl_xor(rs, 32, 64);
+      rs = grp_sum(rs);
       l_run = l_run * alpha + rs;
       m_run = m_new;
 #pragma unroll

@@ -18,8 +18,6 @@
 // per 16 on upload) so no extra HBM pass is spent on them; the normalised projections (QKV,
 // gate/up, logits) scale each output row by its deferred RMSNorm factor (kernels.h RowScale,
 // one tile: rs_rinv(ssq[row])).
-#include <type_traits>
-
 #include "kernels.h"
 
 namespace ms {
@@ -54,73 +52,23 @@ __device__ __forceinline__ void gemm_rs_dma(const RowScale& rs, int M, int m0, f
                                      (LDS_AS void*)(stage + t * BM + r0), 4, 0, 0);
   }
 }
-template <int BM>
+// (every staged load issued before the first add; the adds in tile order)
+template <int BM, int MAXT>
 __device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, const float* stage) {
   if (!rs.ssq || rs.tiles == 1) return;  // block-uniform
   __syncthreads();  // every wave is past its K loop (the DMA landed before the first tile)
   if ((int)threadIdx.x < BM) {
-    float sum = 0.f;
-    for (int t = 0; t < rs.tiles; ++t) sum += stage[t * BM + threadIdx.x];
+    float v[MAXT];
+#pragma unroll
+    for (int t = 0; t < MAXT; ++t) v[t] = t < rs.tiles ? stage[t * BM + threadIdx.x] : 0.f;
+    float sum = v[0];
+#pragma unroll
+    for (int t = 1; t < MAXT; ++t)
+      if (t < rs.tiles) sum += v[t];
     rinv_s[threadIdx.x] = sum;
   }
   __syncthreads();
 }
-// ---- epilogue 4 (prefill QKV): RoPE + K / V scatter.  The output columns of a 16-column group
-// are one tile of a rope-permuted Q / K head (lane fr < 8 holds dim 8t + fr, lane fr + 8 its
-// rotate-half partner 64 + 8t + fr) or 16 dims of a V head.  Per row: its position and cache row
-// once; per element: the fp16-rounded value (rope_kv_kernel's input), the partner by a lane
-// shuffle, rope_kv_kernel's rotation, the store.  Unrolled at compile time (Unroll<>): with
-// runtime loop indices the compiler kept the 128 accumulators of the 256x256 tile in scratch.
-template <int I, int N>
-struct Unroll {
-  template <class F>
-  __device__ __forceinline__ static void run(F&& f) {
-    f(std::integral_constant<int, I>{});
-    Unroll<I + 1, N>::run(f);
-  }
-};
-template <int N>
-struct Unroll<N, N> {
-  template <class F>
-  __device__ __forceinline__ static void run(F&&) {}
-};
-struct RopeRow {
-  int pos;
-  bool valid;
-  size_t kv_off;  // element offset of (page, kv head 0, pos % 64, dim 0) in the cache
-};
-__device__ __forceinline__ RopeRow rope_row(const GemmRope& gp, int row, int M) {
-  RopeRow r;
-  const int rr = min(row, M - 1);
-  r.valid = row < M;
-  r.pos = gp.pos[rr];
-  const KVView& kv = gp.kv;
-  const int page = kv.block_table[(size_t)gp.slot[rr] * kv.max_pages + r.pos / kPage];
-  r.kv_off = ((size_t)page * kv.n_kv_heads * kPage + r.pos % kPage) * kHeadDim;
-  return r;
-}
-__device__ __forceinline__ void gemm_rope_store(const GemmRope& gp, f16_t* qkv, int ldo, int row, const RopeRow& rw,
-                                                int col0, int fr, float a, int N) {
-  const float v = h2f(f2h(a));  // q / k / v rounded to fp16 first: rope_kv_kernel's input
-  const float pv = __shfl_xor(v, 8, 64);
-  const int QD = gp.Hq * kHeadDim, KD = gp.Hk * kHeadDim;
-  if (col0 < QD + KD) {  // wave-uniform
-    const int i = 8 * ((col0 & 127) >> 4) + (fr & 7);
-    const bool lo_lane = fr < 8;
-    const float lo = lo_lane ? v : pv, hi = lo_lane ? pv : v;
-    const float cs = gp.cos_tab[(size_t)rw.pos * 64 + i], sn = gp.sin_tab[(size_t)rw.pos * 64 + i];
-    const float o = lo_lane ? __fsub_rn(__fmul_rn(lo, cs), __fmul_rn(hi, sn))
-                            : __fadd_rn(__fmul_rn(hi, cs), __fmul_rn(lo, sn));
-    const int dim = lo_lane ? i : 64 + i;
-    if (!rw.valid || col0 >= N) return;
-    if (col0 < QD) qkv[(size_t)row * ldo + (col0 & ~127) + dim] = f2h(o);
-    else gp.kv.k[rw.kv_off + (size_t)((col0 - QD) >> 7) * kPage * kHeadDim + dim] = f2h(o);
-  } else {
-    if (!rw.valid || col0 >= N) return;
-    gp.kv.v[rw.kv_off + (size_t)((col0 - QD - KD) >> 7) * kPage * kHeadDim + (col0 & 127) + fr] = f2h(v);
-  }
-}
-
 // ---- the residual epilogue's outputs for the next normalised projection
 __device__ __forceinline__ void gemm_resid_xg(const GemmResid& gr, size_t o, float v, float g, float& ss) {
   float p = v * g;
@@ -153,7 +101,7 @@ template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ A,
                                                      const f16_t* __restrict__ W,
                                                      void* __restrict__ out, int M, int N, int K,
-                                                     int ldo, RowScale rs, GemmResid gr, GemmRope gp) {
+                                                     int ldo, RowScale rs, GemmResid gr) {
   // 64 KiB of tiles + the tile rows' sums of squares (deferred-norm statistics: the folded sum,
   // then up to kGemmRsTiles staged partials).  ONE LDS object: with the DMA into a second array
   // the compiler drained vmcnt before every LDS read
@@ -275,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, m0, n0 / GBN, gr);
     return;
   }
-  gemm_rs_fold<GBM>(rs, rinv_s, rs_stage);
+  gemm_rs_fold<GBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
   f32x4 rv4[4];  // the rows' norm factors, as gemm256_kernel's epilogue
 #pragma unroll
   for (int m = 0; m < 4; ++m) rv4[m] = f32x4{1.f, 1.f, 1.f, 1.f};
@@ -286,18 +234,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     for (int m = 0; m < 4; ++m)
 #pragma unroll
       for (int j = 0; j < 4; ++j) rv4[m][j] = rs_rinv(rv4[m][j], rs);
-  }
-  if constexpr (EPI == kGemmEpiRopeKV) {
-    Unroll<0, 4>::run([&](auto m) {
-      Unroll<0, 4>::run([&](auto j) {
-        const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
-        const RopeRow rw = rope_row(gp, row, M);
-        Unroll<0, 4>::run([&](auto n) {
-          gemm_rope_store(gp, (f16_t*)out, ldo, row, rw, n0 + wn * 64 + n * 16, fr, acc[m][n][(int)j] * rv4[m][(int)j], N);
-        });
-      });
-    });
-    return;
   }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -353,6 +289,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 // c ^ ((r >> 1) & 7) at chunk c -- the 16 rows of a fragment read hit 16 distinct slots of
 // the 256-B bank window (conflict-free); applied on the DMA source and on the read.
 constexpr int TBM = 256, TBN = 256, TBK = 64;
+constexpr int kGemm256RsTiles = 12;  // statistics tiles the 256x256 kernel stages (H / 256 at H = 3072)
 
 __device__ __forceinline__ int swz2(int r) { return (r >> 1) & 7; }
 
@@ -360,11 +297,11 @@ template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict__ A,
                                                         const f16_t* __restrict__ W,
                                                         void* __restrict__ out, int M, int N, int K,
-                                                        int ldo, RowScale rs, GemmResid gr, GemmRope gp) {
+                                                        int ldo, RowScale rs, GemmResid gr) {
   // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics: the folded
   // sum, then up to kGemmRsTiles staged partials).  ONE LDS object: with the DMA into a second
   // array the compiler drained vmcnt before every LDS read
-  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemmRsTiles)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemm256RsTiles)];
   float* rinv_s = (float*)(smem + 2 * 65536);
   float* rs_stage = rinv_s + TBM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -543,7 +480,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
     if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, m0, n0 / TBN, gr);
     return;
   }
-  gemm_rs_fold<TBM>(rs, rinv_s, rs_stage);
+  gemm_rs_fold<TBM, kGemm256RsTiles>(rs, rinv_s, rs_stage);
   // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
   // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
   // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
@@ -557,18 +494,6 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
-  }
-  if constexpr (EPI == kGemmEpiRopeKV) {
-    Unroll<0, 8>::run([&](auto mi) {
-      Unroll<0, 4>::run([&](auto j) {
-        const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
-        const RopeRow rw = rope_row(gp, row, M);
-        Unroll<0, 4>::run([&](auto ni) {
-          gemm_rope_store(gp, (f16_t*)out, ldo, row, rw, n0 + wc * 64 + ni * 16, fr, acc[mi][ni][(int)j] * rv4[mi][(int)j], N);
-        });
-      });
-    });
-    return;
   }
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) {
@@ -611,28 +536,23 @@ static bool gemm_big(int M, int N) {
 int gemm_resid_tiles(int M, int N) { return gemm_big(M, N) ? (N + TBN - 1) / TBN : (N + GBN - 1) / GBN; }
 
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
-                 hipStream_t s, const RowScale* rs_in, const GemmResid* gr_in, const GemmRope* gp_in) {
+                 hipStream_t s, const RowScale* rs_in, const GemmResid* gr_in) {
   if (M <= 0) return;
+  const bool big = gemm_big(M, N);
   RowScale rs{};
   if (rs_in && rs_in->ssq && epi != 1) {
-    if (rs_in->tiles < 1 || rs_in->tiles > kGemmRsTiles) return;  // callers check (ms_op_gemm)
+    if (rs_in->tiles < 1 || rs_in->tiles > (big ? kGemm256RsTiles : kGemmRsTiles)) return;  // callers check
     rs = *rs_in;
   }
   GemmResid gr{};
   if (gr_in && epi == 1) gr = *gr_in;
-  GemmRope gp{};
-  if (epi == kGemmEpiRopeKV) {
-    if (!gp_in || N % 16) return;  // callers pass the token positions and the cache
-    gp = *gp_in;
-  }
-#define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr, gp)
-  if (gemm_big(M, N)) {
+#define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr)
+  if (big) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {
       case 0: GL(gemm256_kernel, 0, 512); break;
       case 1: GL(gemm256_kernel, 1, 512); break;
       case 2: GL(gemm256_kernel, 2, 512); break;
-      case kGemmEpiRopeKV: GL(gemm256_kernel, kGemmEpiRopeKV, 512); break;
       default: GL(gemm256_kernel, 3, 512); break;
     }
     return;
@@ -642,10 +562,13 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
     case 0: GL(gemm_kernel, 0, 256); break;
     case 1: GL(gemm_kernel, 1, 256); break;
     case 2: GL(gemm_kernel, 2, 256); break;
-    case kGemmEpiRopeKV: GL(gemm_kernel, kGemmEpiRopeKV, 256); break;
     default: GL(gemm_kernel, 3, 256); break;
   }
 #undef GL
+}
+
+bool gemm_rs_tiles_ok(int M, int N, int tiles) {
+  return tiles >= 1 && tiles <= (gemm_big(M, N) ? kGemm256RsTiles : kGemmRsTiles);
 }
 
 }  // namespace ms

@@ -88,24 +88,13 @@ struct GemmResid {
   f16_t* xg;
   float* ssq;
 };
-constexpr int kGemmRsTiles = 24;
-// epilogue 4 (prefill QKV, weight rows rope-permuted as for the decode GEMV): q / k / v rounded to
-// fp16, RoPE on the Q / K heads (rope_kv_kernel's arithmetic), Q stored in natural order into the
-// output rows, K / V scattered into the paged cache -- no rope_kv launch
-constexpr int kGemmEpiRopeKV = 4;
-struct GemmRope {
-  const int32_t* pos;   // [M] token positions
-  const int32_t* slot;  // [M] block-table rows
-  const float* cos_tab;
-  const float* sin_tab;
-  KVView kv;
-  int Hq, Hk;
-};
+constexpr int kGemmRsTiles = 24;  // the 128-column kernel's count at H = 3072 (the 256-column one: 12)
 // statistics tiles the residual epilogue writes for an M x N GEMM (its column-tile count)
 int gemm_resid_tiles(int M, int N);
+// whether an M x N GEMM's row scale can fold `tiles` statistics tiles (launch_gemm skips otherwise)
+bool gemm_rs_tiles_ok(int M, int N, int tiles);
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo,
-                 int epi, hipStream_t s, const RowScale* rs = nullptr, const GemmResid* gr = nullptr,
-                 const GemmRope* gp = nullptr);
+                 int epi, hipStream_t s, const RowScale* rs = nullptr, const GemmResid* gr = nullptr);
 // tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
 void set_gemm_variant(int v);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.

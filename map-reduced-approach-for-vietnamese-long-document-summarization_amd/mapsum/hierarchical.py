@@ -1,15 +1,15 @@
 """Hierarchical summarisation with level-synchronous batching.
 
 Follows runners/run_summarization_ollama_mapreduce_hierarchical.py:
-  collapse_level (:226-258)            every non-Paragraph node at one depth is summarised
+  collapse_level (:242-274)            every non-Paragraph node at one depth is summarised
                                        and replaced by a Paragraph "title:\\nsummary"
   summarize_text_mapreduce (:168-199)  split (RecursiveCharacterTextSplitter, word-count
                                        length, :178-186) -> map each chunk -> one reduce
-  hierarchical_summarize_document (:261-315)  depths deepest..1, then the whole document,
+  hierarchical_summarize_document (:277-315)  depths deepest..1, then the whole document,
                                        then one review/polish call
 
 The reference awaits every target, and every chunk inside a target, one after another
-(:151-160, :232-256).  All of them are independent, so here one depth is one batch: every
+(:132-141, :248-274).  All of them are independent, so here one depth is one batch: every
 map prompt of every target at that depth is issued together, then every reduce prompt.
 The engine is greedy and batch-invariant (one decode arithmetic per engine,
 whatever the number of sequences in flight), so each call returns the string it would have
@@ -142,7 +142,7 @@ class RecursiveCharacterTextSplitter:
         return self._split(text, self.separators)
 
 
-# ---------------------------------------------------------------- tree helpers (:201-224)
+# ---------------------------------------------------------------- tree helpers (:202-240)
 def depth_first_traverse(node: dict, callback, depth: int = 0, parent=None):
     callback(node, depth, parent)
     for child in node.get("children", []):
@@ -196,7 +196,7 @@ async def summarize_texts_mapreduce(texts: list, llm, *, chunk_size: int = 12000
 
 async def collapse_level(root: dict, depth_level: int, llm, chunk_size: int = 12000,
                          chunk_overlap: int = 200) -> int:
-    """:226-258 with the targets of one depth summarised as one batch."""
+    """:242-274 with the targets of one depth summarised as one batch."""
     targets = collect_nodes_at_depth(root, depth_level)
     work = []
     for t in targets:
@@ -215,7 +215,7 @@ async def collapse_level(root: dict, depth_level: int, llm, chunk_size: int = 12
 
 async def hierarchical_summarize_document(document_node: dict, *, max_depth: int, llm,
                                           chunk_size: int = 12000, chunk_overlap: int = 200) -> str:
-    """:261-315: collapse deepest..1, summarise the document, then one review call."""
+    """:277-315: collapse deepest..1, summarise the document, then one review call."""
     for d in range(min(max_depth, tree_depth(document_node)), 0, -1):
         await collapse_level(document_node, d, llm, chunk_size, chunk_overlap)
     final_text = extract_descendant_paragraph_text(document_node)

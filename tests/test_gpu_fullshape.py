@@ -357,7 +357,11 @@ def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
         else:
             gen = np.asarray(e.generate([prompt], num_predict=64, ignore_eos=True)[0].ids)
         _Q4_GEN[slots] = gen
-        if 2 in _Q4_GEN:  # engine-size invariance: the K-quant arithmetic is per row
+        if 2 in _Q4_GEN and slots == 32:
+            # engine-size invariance: the K-quant GEMV arithmetic is per row, and 2- and 32-slot
+            # engines share the decode-attention plan (2 pages per wave); a 128-slot engine splits
+            # attention at 8 pages per wave (attn_decode_ppw), a different fp32 sum order, so
+            # there only the oracle check below applies
             assert np.array_equal(gen, _Q4_GEN[2]), (slots, np.nonzero(gen != _Q4_GEN[2])[0][:5])
         tl = _teacher_forced(o, cache, ref_lg[-1], gen)
         want = np.argmax(tl, 1)

@@ -3,7 +3,8 @@
     python tools/bench_kernels.py gemv [--m 8]
     python tools/bench_kernels.py gemm
 
-Times each launch with HIP events on the launch stream (median of interleaved rounds),
+Operands are fp16 (the engine's storage type).  Times each launch with HIP events on the
+launch stream (median of interleaved rounds),
 reports algorithmic GB/s (gemv: weight + activation bytes) or TFLOP/s (gemm).
 """
 import argparse
@@ -42,10 +43,10 @@ def bench_gemv(lib, M, shapes, waves_list):
     # a 1 GB buffer swept between rounds keeps weights out of the 256 MB MALL
     flush = torch.empty(256 * 1024 * 1024, dtype=torch.float32, device=dev)
     for name, N, K, epi in shapes:
-        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02 for _ in range(8)]
-        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        Ws = [torch.randn(N, K, device=dev).to(torch.float16) * 0.02 for _ in range(8)]
+        X = torch.randn(M, K, device=dev).to(torch.float16)
         out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
-                          dtype=torch.float32 if epi in (1, 3) else torch.bfloat16)
+                          dtype=torch.float32 if epi in (1, 3) else torch.float16)
         ldo = N if epi != 2 else N // 2
         byts = N * K * 2 + M * K * 2 + out.numel() * out.element_size() * (2 if epi == 1 else 1)
         line = f"{name:8s} N={N:6d} K={K:5d} M={M:3d} {byts/1e6:8.1f} MB |"
@@ -75,9 +76,9 @@ def bench_split(lib, M):
     for name, N, K in [("o", 3072, 3072), ("down", 3072, 8192), ("qkv", 5120, 3072)]:
         # enough weight copies that the rotation streams > 512 MB: the 256 MB MALL never
         # holds the matrix a launch reads (as in a decode step, which streams 6.4 GB)
-        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02
+        Ws = [torch.randn(N, K, device=dev).to(torch.float16) * 0.02
               for _ in range(max(8, -(-512 * 2**20 // (N * K * 2))))]
-        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        X = torch.randn(M, K, device=dev).to(torch.float16)
         slabs = torch.zeros(8, M, N, device=dev)
         for S in (1, 2, 3, 4, 6, 8):
             byts = N * K * 2 + M * K * 2 + S * M * N * 4
@@ -109,10 +110,10 @@ def bench_dgemm(lib):
     for name, N, K, epi, splits in [("qkv", 5120, 3072, 3, (1, 2, 3, 6)), ("o", 3072, 3072, 3, (1, 2, 4, 6)),
                                     ("gu", 16384, 3072, 2, (1,)), ("down", 3072, 8192, 3, (1, 2, 4, 8)),
                                     ("lm_head", 128256, 3072, 5, (1,))]:
-        Ws = [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02
+        Ws = [torch.randn(N, K, device=dev).to(torch.float16) * 0.02
               for _ in range(max(2, -(-512 * 2**20 // (N * K * 2))))]
         for M in (8, 16, 32, 64, 128, 256):
-            X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+            X = torch.randn(M, K, device=dev).to(torch.float16)
             out = torch.zeros(8 * M * N, device=dev)
             wbytes = N * K * 2
             line = f"{name:7s} N={N:6d} K={K:5d} M={M:3d} |"
@@ -161,14 +162,14 @@ def bench_qgemv(lib, M):
         pks = []
         for _ in range(max(2, -(-512 * 2**20 // nbytes))):
             pk = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            wbf = torch.empty(rows_src, K, dtype=torch.bfloat16, device=dev)
+            wbf = torch.empty(rows_src, K, dtype=torch.float16, device=dev)
             for r0 in range(0, N, rows_src):  # tile the random rows over the matrix
                 rr = min(rows_src, N - r0)
                 tmp = torch.empty(rr * (K // 256) * bpb, dtype=torch.uint8, device=dev)
                 lib.ms_op_quant_rows(qt, bd.data_ptr(), rr, K, wbf.data_ptr(), tmp.data_ptr(), st)
                 pk[r0 * (K // 256) * bpb:(r0 + rr) * (K // 256) * bpb] = tmp
             pks.append(pk)
-        X = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        X = torch.randn(M, K, device=dev).to(torch.float16)
         out = torch.zeros(8 * M * N, device=dev)
         ldo = N // 2 if epi == 2 else N
         i = [0]
@@ -199,9 +200,9 @@ def bench_camp(lib, M):
         line = f"{name:8s} N={N:6d} K={K:5d} M={M:2d} |"
         for pad in (0, 64, 128, 256, 512):
             ldk = K + pad
-            Ws = [torch.randn(N, ldk, device=dev).to(torch.bfloat16) * 0.02
+            Ws = [torch.randn(N, ldk, device=dev).to(torch.float16) * 0.02
                   for _ in range(max(2, -(-512 * 2**20 // (N * ldk * 2))))]
-            X = torch.randn(M, ldk, device=dev).to(torch.bfloat16)
+            X = torch.randn(M, ldk, device=dev).to(torch.float16)
             out = torch.zeros(M, N, device=dev)
             i = [0]
 
@@ -225,11 +226,11 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0):
     ssq = (torch.rand(16384, device=dev) * 3072 + 1.0).float()
     for name, M, N, K, epi in [("qkv", 16384, 5120, 3072, 0), ("o", 16384, 3072, 3072, 1),
                                ("gu", 16384, 16384, 3072, 2), ("down", 16384, 3072, 8192, 1),
-                               ("sq4k", 4096, 4096, 4096, 0)]:
-        A = ((torch.rand(M, K, device=dev) * 2 - 1) * ascale).to(torch.bfloat16)
-        W = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+                               ("sq4k", 4096, 4096, 4096, 0), ("sq8k", 8192, 8192, 8192, 0)]:
+        A = ((torch.rand(M, K, device=dev) * 2 - 1) * ascale).to(torch.float16)
+        W = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.float16)
         out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
-                          dtype=torch.float32 if epi in (1, 3) else torch.bfloat16)
+                          dtype=torch.float32 if epi in (1, 3) else torch.float16)
         ldo = N if epi != 2 else N // 2
 
         def fn():

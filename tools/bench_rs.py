@@ -29,7 +29,7 @@ def main():
     has_resid = hasattr(lib, "ms_op_gemv_resid")
 
     def rot(N, K):
-        return [torch.randn(N, K, device=dev).to(torch.bfloat16) * 0.02
+        return [torch.randn(N, K, device=dev).to(torch.float16) * 0.02
                 for _ in range(max(4, -(-512 * 2**20 // (N * K * 2))))]
 
     def run(tag, fn, byts):
@@ -38,8 +38,8 @@ def main():
 
     # gate/up + SwiGLU
     Wg = rot(2 * F, H)
-    X = torch.randn(M, H, device=dev).to(torch.bfloat16)
-    h = torch.empty(M, F, dtype=torch.bfloat16, device=dev)
+    X = torch.randn(M, H, device=dev).to(torch.float16)
+    h = torch.empty(M, F, dtype=torch.float16, device=dev)
     i = [0]
 
     def gu():
@@ -63,12 +63,12 @@ def main():
     run("qkv split6", qkv, 5120 * H * 2)
     # O / down: slabs + residual_rmsnorm vs the fused residual epilogue
     x = torch.randn(M, H, device=dev)
-    g = torch.ones(H, dtype=torch.bfloat16, device=dev)
-    xb = torch.empty(M, H, dtype=torch.bfloat16, device=dev)
+    g = torch.ones(H, dtype=torch.float16, device=dev)
+    xb = torch.empty(M, H, dtype=torch.float16, device=dev)
     ssq = torch.empty(256, M, device=dev)
     for name, K, S in (("o", H, 6), ("down", F, 4)):
         Wo = rot(H, K)
-        Xo = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        Xo = torch.randn(M, K, device=dev).to(torch.float16)
 
         def split():
             i[0] += 1
