@@ -82,7 +82,7 @@ __device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x
 // MFMAs -- the round-3 kernel (4 waves x 16 rows, hi + lo bf16 P) held 240 VGPRs + 148 AGPRs at
 // one wave per SIMD and could not hide its own QK -> softmax -> PV chain.  The online softmax
 // works on raw scores (p = exp2(s*c - m*c), c = log2(e)/sqrt(d)) with a lazily moved reference
-// max (below), so the O rescale factor is exactly 1 on most tiles; the causal /
+// max (below); the O rescale is skipped when no query column of the wave moved it; the causal /
 // sequence-end mask is applied only on tiles that can cross it, and a wave skips the tiles that
 // lie wholly after its last query.  K/V tiles reach LDS by DMA (global_load_lds, no register
 // staging and no ds_write), two buffers: tile t+1 is in flight while tile t is multiplied, one
@@ -201,6 +201,7 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
         }
     }
     f16x8 pf[GB][2];
+    bool rescale = false;
     float alpha[GB];
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh) {
@@ -218,6 +219,7 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       const bool grow = m_new != m_run[hh] && !((m_new - m_run[hh]) * scale_log2 <= 8.f);
       const float m_use = grow ? m_new : m_run[hh];
       alpha[hh] = grow ? __builtin_amdgcn_exp2f((m_run[hh] - m_new) * scale_log2) : 1.f;
+      rescale |= grow;
       const float mc = (m_use == -INFINITY) ? 0.f : m_use * scale_log2;
       float rs = 0.f;
 #pragma unroll
@@ -234,12 +236,14 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       pf[hh][0] = pack_p(sc[hh][0], sc[hh][1]);
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
     }
-    // unconditional (alpha = 1 exactly unless the reference max moved): a branch here split
-    // the tile into basic blocks the scheduler could not interleave MFMA and VALU across
+    // (an unconditional multiply -- alpha = 1 exactly unless the max moved -- measured
+    // slower: 312 vs 297 us per layer, profiles/r04/v6_*)
+    if (__ballot(rescale) != 0) {
 #pragma unroll
-    for (int hh = 0; hh < GB; ++hh)
+      for (int hh = 0; hh < GB; ++hh)
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) o[hh][dt] *= alpha[hh];
+        for (int dt = 0; dt < 8; ++dt) o[hh][dt] *= alpha[hh];
+    }
 #pragma unroll
     for (int kstep = 0; kstep < 2; ++kstep)
 #pragma unroll

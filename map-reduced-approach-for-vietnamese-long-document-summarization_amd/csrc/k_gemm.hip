@@ -283,7 +283,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 //   phase 0: UAb(t+1)  phase 1: UBl(t+1)  phase 2: UAt(t+2)  phase 3: UBr(t+2)
 // then phase 3 waits vmcnt(4): everything up to UBl(t+1) has landed while UAt/UBr(t+2)
 // stay in flight across the barrier (never vmcnt(0) in the steady state).  Tile t+1 is
-// first read in the next phase, after a barrier.  The two wave rows run one barrier apart
+// first read in the next phase, after a barrier.  (A deeper form -- reads retired before each
+// phase's first barrier, restaging one phase after the last read, vmcnt(6) with three units
+// in flight -- measured neutral, 1284 vs 1280 TF/s at 8192^3: the loop is not latency-bound.
+// On uniform random fp16 it runs 1286 TF/s at 8192^3 and 1706 on zero A (the clock under
+// MFMA power), profiles/r04/v7_*.)  The two wave rows run one barrier apart
 // (wave row 1 takes an extra s_barrier up front), so one row's MFMA cluster overlaps the
 // other row's LDS reads and DMA issue.  LDS swizzle: row r holds global 16-B chunk
 // c ^ ((r >> 1) & 7) at chunk c -- the 16 rows of a fragment read hit 16 distinct slots of

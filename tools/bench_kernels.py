@@ -218,7 +218,14 @@ def bench_camp(lib, M):
         print(line, flush=True)
 
 
-def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0):
+def _trunc(x, bits):
+    """fp16 tensor with the low `bits` mantissa bits cleared (bits = 3: bf16-like precision)"""
+    if bits <= 0:
+        return x
+    return (x.view(torch.int16) & ~((1 << bits) - 1)).view(torch.float16)
+
+
+def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0):
     """rs: the normalised projections (epi 0 / 2) take a one-tile deferred-norm row scale, as
     in prefill (ms_op_set_row_scale; needs a library that has it)"""
     dev = torch.device("cuda:0")
@@ -227,8 +234,8 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0):
     for name, M, N, K, epi in [("qkv", 16384, 5120, 3072, 0), ("o", 16384, 3072, 3072, 1),
                                ("gu", 16384, 16384, 3072, 2), ("down", 16384, 3072, 8192, 1),
                                ("sq4k", 4096, 4096, 4096, 0), ("sq8k", 8192, 8192, 8192, 0)]:
-        A = ((torch.rand(M, K, device=dev) * 2 - 1) * ascale).to(torch.float16)
-        W = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.float16)
+        A = _trunc(((torch.rand(M, K, device=dev) * 2 - 1) * ascale).to(torch.float16), trunc)
+        W = _trunc((torch.rand(N, K, device=dev) * 2 - 1).to(torch.float16), trunc)
         out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
                           dtype=torch.float32 if epi in (1, 3) else torch.float16)
         ldo = N if epi != 2 else N // 2
@@ -250,6 +257,7 @@ if __name__ == "__main__":
     ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp"])
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--ascale", type=float, default=1.0, help="gemm: scale of the uniform A entries")
+    ap.add_argument("--trunc", type=int, default=0, help="gemm: clear this many low mantissa bits of A and W")
     ap.add_argument("--rs", action="store_true", help="gemm: deferred-norm row scale on epi 0 / 2")
     ap.add_argument("--variants", default="1,2", help="gemm: tile variants (1: 128x128, 2: 256x256)")
     a = ap.parse_args()
@@ -267,4 +275,4 @@ if __name__ == "__main__":
     elif a.what == "camp":
         bench_camp(lib, a.m)
     else:
-        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale)
+        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc)
