@@ -272,8 +272,13 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
+    def note(msg):  # progress on stderr (rank 0): long runs must not look hung
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+    note(f"engine ready (B={B}, weights {args.weights}, load {t_load:.1f} s)")
     for _ in range(args.warmup):
         one_step()
+    note(f"{args.warmup} warmup step(s) done")
     eng.reset_stats()
     gather_s[0] = 0.0
     outs = []
@@ -383,6 +388,7 @@ def main():
         "check": check,
         "cpu_baseline": None,
     }
+    note(f"timed {args.steps} step(s): {value:.3f} chunks/s")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         eng.close()
         out["cpu_baseline"] = cpu_baseline(cfg, chunks[0], args.gen_len)

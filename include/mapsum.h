@@ -211,7 +211,7 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
                int32_t ldo, int32_t epilogue, void* stream);
 /* prefill O / down with the residual update fused (the engine's prefill layer): x fp32 [M][N] +=
    A . W^T, and the input of the next normalised projection: xg_out fp16 [M][N] = f16(x * gamma),
-   ssq_out fp32 [tiles][M] = per-column-tile sums of the new x^2 (tiles = ms_gemm_resid_tiles(M, N)),
+   ssq_out fp32 [tiles][M] = per-128-column sums of the new x^2 (tiles = ms_gemm_resid_tiles(M, N) = N / 128),
    the deferred RMSNorm statistics the next ms_op_gemm takes through ms_op_set_row_scale */
 int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const void* gamma, float* ssq_out,
                      int32_t M, int32_t N, int32_t K, void* stream);

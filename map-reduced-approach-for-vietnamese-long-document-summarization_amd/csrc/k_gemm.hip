@@ -76,12 +76,16 @@ __device__ __forceinline__ void gemm_resid_xg(const GemmResid& gr, size_t o, flo
   gr.xg[o] = f2h(p);
   ss += v * v;
 }
-// per-row sums of x^2 over the block's BN columns: lane partials (its NI columns, in order) ->
-// LDS [row][wave column][lane column] -> one thread per row adds them in order.  The tile
-// buffers are free: every wave is past its K loop.
+// per-row sums of x^2 per 128-column group of the block (the statistics tile: kGemmStatCols,
+// the same on both GEMM tiles, so a row's statistics -- and its deferred-norm scale -- never
+// depend on which tile the packed prompt length picked): lane partials (its NI columns, in
+// order) -> LDS [row][wave column][lane column] -> one thread per (row, group) adds its two
+// wave columns' 32 partials in order.  The tile buffers are free: every wave is past its K loop.
 template <int BM, int WCOLS, int MI>
 __device__ __forceinline__ void gemm_resid_ssq(char* smem, const float (&ss)[MI][4], int wrow0, int wcol,
-                                               int fg, int fr, int M, int m0, int tile, const GemmResid& gr) {
+                                               int fg, int fr, int M, int N, int m0, int n0, const GemmResid& gr) {
+  static_assert(WCOLS % 2 == 0, "a statistics group is two 64-column wave columns");
+  constexpr int G = WCOLS / 2;
   float* red = (float*)smem;
   __syncthreads();
 #pragma unroll
@@ -89,11 +93,13 @@ __device__ __forceinline__ void gemm_resid_ssq(char* smem, const float (&ss)[MI]
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[((wrow0 + mi * 16 + fg * 4 + j) * WCOLS + wcol) * 16 + fr] = ss[mi][j];
   __syncthreads();
-  if ((int)threadIdx.x < BM && m0 + (int)threadIdx.x < M) {
-    const float* p = red + threadIdx.x * WCOLS * 16;
+  for (int t = threadIdx.x; t < BM * G; t += blockDim.x) {
+    const int row = t % BM, grp = t / BM;
+    if (m0 + row >= M || n0 + grp * kGemmStatCols >= N) continue;
+    const float* p = red + row * WCOLS * 16 + grp * 32;
     float sum = 0.f;
-    for (int q = 0; q < WCOLS * 16; ++q) sum += p[q];
-    gr.ssq[(size_t)tile * M + m0 + threadIdx.x] = sum;
+    for (int q = 0; q < 32; ++q) sum += p[q];
+    gr.ssq[(size_t)(n0 / kGemmStatCols + grp) * M + m0 + row] = sum;
   }
 }
 
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
             }
           }
     }
-    if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, m0, n0 / GBN, gr);
+    if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, N, m0, n0, gr);
     return;
   }
   gemm_rs_fold<GBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
@@ -293,7 +299,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 // c ^ ((r >> 1) & 7) at chunk c -- the 16 rows of a fragment read hit 16 distinct slots of
 // the 256-B bank window (conflict-free); applied on the DMA source and on the read.
 constexpr int TBM = 256, TBN = 256, TBK = 64;
-constexpr int kGemm256RsTiles = 12;  // statistics tiles the 256x256 kernel stages (H / 256 at H = 3072)
 
 __device__ __forceinline__ int swz2(int r) { return (r >> 1) & 7; }
 
@@ -305,7 +310,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   // two K-tile buffers + the tile rows' sums of squares (deferred-norm statistics: the folded
   // sum, then up to kGemmRsTiles staged partials).  ONE LDS object: with the DMA into a second
   // array the compiler drained vmcnt before every LDS read
-  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemm256RsTiles)];
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemmRsTiles)];
   float* rinv_s = (float*)(smem + 2 * 65536);
   float* rs_stage = rinv_s + TBM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -481,10 +486,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
             }
           }
     }
-    if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, m0, n0 / TBN, gr);
+    if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, N, m0, n0, gr);
     return;
   }
-  gemm_rs_fold<TBM, kGemm256RsTiles>(rs, rinv_s, rs_stage);
+  gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
   // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
   // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
   // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
@@ -537,7 +542,10 @@ static bool gemm_big(int M, int N) {
   return g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
 }
 
-int gemm_resid_tiles(int M, int N) { return gemm_big(M, N) ? (N + TBN - 1) / TBN : (N + GBN - 1) / GBN; }
+int gemm_resid_tiles(int M, int N) {
+  (void)M;
+  return (N + kGemmStatCols - 1) / kGemmStatCols;
+}
 
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  hipStream_t s, const RowScale* rs_in, const GemmResid* gr_in) {
@@ -545,7 +553,7 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
   const bool big = gemm_big(M, N);
   RowScale rs{};
   if (rs_in && rs_in->ssq && epi != 1) {
-    if (rs_in->tiles < 1 || rs_in->tiles > (big ? kGemm256RsTiles : kGemmRsTiles)) return;  // callers check
+    if (rs_in->tiles < 1 || rs_in->tiles > kGemmRsTiles) return;  // callers check
     rs = *rs_in;
   }
   GemmResid gr{};
@@ -572,7 +580,9 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
 }
 
 bool gemm_rs_tiles_ok(int M, int N, int tiles) {
-  return tiles >= 1 && tiles <= (gemm_big(M, N) ? kGemm256RsTiles : kGemmRsTiles);
+  (void)M;
+  (void)N;
+  return tiles >= 1 && tiles <= kGemmRsTiles;
 }
 
 }  // namespace ms

@@ -82,14 +82,16 @@ void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream
 // statistics, or null): the deferred RMSNorm scale of the output rows (epilogues 0, 2, 3).
 // gr (epilogue 1, the residual add of O / down): the GEMM also writes the next normalised
 // projection's input, gr->xg = f16(x_new * gr->gamma) [M][N], and per-tile sums of x_new^2,
-// gr->ssq [N / tile][M] (tile = the kernel's column tile; gemm_resid_tiles) -- no norm launch.
+// gr->ssq [N / 128][M] (gemm_resid_tiles) -- no norm launch.
 struct GemmResid {
   const f16_t* gamma;
   f16_t* xg;
   float* ssq;
 };
-constexpr int kGemmRsTiles = 24;  // the 128-column kernel's count at H = 3072 (the 256-column one: 12)
-// statistics tiles the residual epilogue writes for an M x N GEMM (its column-tile count)
+constexpr int kGemmRsTiles = 24;     // statistics tiles a consumer GEMM folds (H / 128 at H = 3072)
+constexpr int kGemmStatCols = 128;  // columns per statistics tile, on both GEMM tiles
+// statistics tiles the residual epilogue writes for an M x N GEMM: N / 128 whatever the tile,
+// so a packed prompt's rows get the same statistics at any packing (batch invariance)
 int gemm_resid_tiles(int M, int N);
 // whether an M x N GEMM's row scale can fold `tiles` statistics tiles (launch_gemm skips otherwise)
 bool gemm_rs_tiles_ok(int M, int N, int tiles);

@@ -106,8 +106,9 @@ class TorchCpuLlama:
         return (xg @ W.T).float() * r
 
     @torch.inference_mode()
-    def forward(self, ids, cache, p0):
-        """ids [T] after p0 cached tokens; returns the last position's greedy id."""
+    def forward(self, ids, cache, p0, progress=None):
+        """ids [T] after p0 cached tokens; returns the last position's greedy id.  progress(l):
+        called after each layer (long CPU prefills report as they go)."""
         cfg = self.cfg
         T = ids.shape[0]
         D, Hq, Hk = cfg.head_dim, cfg.n_heads, cfg.n_kv_heads
@@ -128,6 +129,8 @@ class TorchCpuLlama:
             gu = self._proj(x, L["n2"], L["wgu"])
             h = F.silu(gu[:, :cfg.ffn].float()) * gu[:, cfg.ffn:].float()
             x = x + (h.to(self.dt) @ L["wdown"].T).float()
+            if progress is not None:
+                progress(l)
         self.last_logits = self._proj(x[-1:], self.final_norm, self.lm_head)[0]
         return int(torch.argmax(self.last_logits))
 
@@ -152,17 +155,27 @@ def time_chunk(cfg, prompt_ids, gen_len: int, decode_sample: int = 16, seed: int
     ``decode_sample`` greedy decode steps, extrapolated to ``gen_len`` generated tokens
     (decode steps at this context length cost the same to within the KV growth).  The weights
     are the engine's (bench.py: ms_init_synthetic(seed 0, std 0.02, jitter 0))."""
+    import sys
+
+    def note(msg):  # progress on stderr: a GPU-box run that prints nothing for minutes looks hung
+        print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
+    t0 = time.perf_counter()
     m = TorchCpuLlama(cfg, seed=seed, std=std)
+    note(f"weights built in {time.perf_counter() - t0:.1f} s, {torch.get_num_threads()} threads")
     ids = torch.as_tensor(prompt_ids, dtype=torch.long)
     P = ids.shape[0]
     cache = m.new_cache(P + gen_len)
     t0 = time.perf_counter()
-    tok = m.forward(ids, cache, 0)
+    tok = m.forward(ids, cache, 0, progress=lambda l: (l + 1) % 7 == 0 and note(
+        f"prefill layer {l + 1}/{cfg.n_layers}: {time.perf_counter() - t0:.1f} s"))
     t_pre = time.perf_counter() - t0
+    note(f"prefill of {P} tokens: {t_pre:.1f} s")
     n = min(decode_sample, gen_len - 1)
     t0 = time.perf_counter()
     for i in range(n):
         tok = m.forward(torch.tensor([tok]), cache, P + i)
+        if (i + 1) % 16 == 0:
+            note(f"decode step {i + 1}/{n}: {(time.perf_counter() - t0) / (i + 1) * 1e3:.1f} ms/step")
     t_dec = (time.perf_counter() - t0) / max(n, 1)
     chunk_s = t_pre + (gen_len - 1) * t_dec
     return {"prefill_s": t_pre, "decode_step_s": t_dec, "chunk_s": chunk_s,

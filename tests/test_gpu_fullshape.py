@@ -420,6 +420,29 @@ def test_config2_continuous_batching_full_width(oracle):
         e.close()
 
 
+def test_prefill_packing_invariance(dev):
+    """A prompt's prefill does not depend on what it is packed with: alone (600 rows: the
+    128x128 GEMM tile) and behind a 1500-token prompt (2100 rows: the 256x256 tile) its hidden
+    states after every layer are bitwise equal, and so are its greedy tokens -- the prefill
+    residual epilogue writes its norm statistics per 128 columns on both tiles (round 4 first
+    wrote them per column tile, and configs[3]'s ragged batch-invariance check caught it)."""
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, 128000, size=600).astype(np.int32)
+    b = rng.integers(0, 128000, size=1500).astype(np.int32)
+    e = Engine(CFG, device=0, max_batch=2, max_ctx=2048, max_prefill_tokens=4096)
+    try:
+        e.init_synthetic(SEED, STD, JIT)
+        for nl in range(1, CFG.n_layers + 1):
+            h1, _ = e.forward_packed([a], n_layers=nl)
+            h2, _ = e.forward_packed([b, a], n_layers=nl)
+            assert np.array_equal(h1, h2[len(b):]), nl
+        alone = e.generate([a], num_predict=16, ignore_eos=True)[0].ids
+        both = e.generate([b, a], num_predict=16, ignore_eos=True)[1].ids
+        assert alone == both
+    finally:
+        e.close()
+
+
 @pytest.mark.timeout(1200)
 def test_config3_ragged_sections_full_width(oracle):
     """BASELINE configs[3] at full width (2 layers): ragged hierarchical sections of 64, 611,

@@ -70,7 +70,7 @@ def main():
         "config": {"sections": args.sections, "max_batch": args.max_batch, "gen_len": args.gen_len,
                    "prompt_tokens": {"min": int(lens.min()), "median": int(np.median(lens)),
                                      "max": int(lens.max()), "sum": int(lens.sum())},
-                   "weights": "bf16 synthetic", "n_gpus": 1},
+                   "weights": "f16 synthetic", "n_gpus": 1},
         "graphs_built": st["graphs_built"], "check": check}), flush=True)
 
 

@@ -3,7 +3,7 @@
 # and without a natural-EOS stop set) and configs[3] (ragged hierarchical level).  Each step has
 # its own limit and the chain stops at the first failure.
 export TMPDIR=/tmp; mkdir -p gpurun_out; O=gpurun_out; R=/tmp/mscfg; rm -rf $R; mkdir -p $R
-timeout -k 10 400 python -u bench.py --weights q4_k_m > $O/bench_q4_k_m.json 2> $O/bench_q4_k_m.err || { tail -20 $O/bench_q4_k_m.err; exit 1; }
+timeout -k 10 400 python -u bench.py --weights q4_k_m --no-cpu-baseline > $O/bench_q4_k_m.json 2> $O/bench_q4_k_m.err || { tail -20 $O/bench_q4_k_m.err; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/prof -o run -- python3 bench.py --weights q4_k_m --no-cpu-baseline --no-check --no-roofline > $O/prof_bench_q4_k_m.json 2> $R/prof.err || { tail -20 $R/prof.err; exit 1; }
 python3 tools/prof_summary.py "$(find $R/prof -name '*kernel_stats.csv' | head -n 1)" > $O/kernel_stats_q4_k_m.txt
 timeout -k 10 400 python -u bench.py --docs 32 --max-batch 128 --steps 1 --warmup 1 --no-cpu-baseline > $O/config2_B128.json 2> $O/config2.err || { tail -20 $O/config2.err; exit 1; }
