@@ -112,24 +112,39 @@ def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=64):
     bf16 restatement of the same map call (oracle/torch_cpu.py), all 28 layers, on one
     chunk of this workload: its full 2048-token prefill + ``decode_sample`` greedy decode
     steps, extrapolated to the 256 generated tokens.  Threads: every CPU this process may
-    run on (its affinity mask -- BASELINE.md §2 asks for num_thread = physical cores; the
-    sample text records both counts)."""
+    run on -- its affinity mask capped by its cgroup CPU quota (BASELINE.md §2 asks for
+    num_thread = physical cores; the sample text records the mask, the quota and the host's
+    physical cores)."""
     import torch
     from oracle.torch_cpu import time_chunk
     allowed = len(os.sched_getaffinity(0))
-    torch.set_num_threads(allowed)
+    quota = _cgroup_cpus()
+    # every CPU this process can actually run on: the affinity mask, capped by the cgroup CPU
+    # quota (a GPU box's share of a big host shows every host CPU in the mask; threads past
+    # the quota only oversubscribe it)
+    threads = min(allowed, quota) if quota else allowed
+    torch.set_num_threads(threads)
     phys = _physical_cores()
     r = time_chunk(cfg, prompt_ids, gen_len, decode_sample=decode_sample)
     return {"value": round(1.0 / r["chunk_s"], 5), "unit": "chunks/s", "cores": int(r["threads"]),
             "kind": "port", "cpu_model": r["cpu_model"],
             "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16 on {r['cpu_model']}, "
-                       f"{r['threads']} threads = every CPU of this process's affinity mask ({allowed}; "
-                       f"{phys} physical cores on the host), "
+                       f"{r['threads']} threads = every CPU this process may use (affinity mask {allowed}, "
+                       f"cgroup quota {quota if quota else 'none'}; {phys} physical cores on the host), "
                        f"{cfg.n_layers}-layer Llama-3.2-3B on the engine's own synthetic weights, "
                        f"1 chunk: {len(prompt_ids)}-tok prefill "
                        f"{r['prefill_s']:.2f} s + {r['decode_steps_timed']} decode steps at "
                        f"{r['decode_step_s'] * 1e3:.1f} ms, extrapolated to {gen_len} tokens "
                        f"({r['chunk_s']:.1f} s/chunk)")}
+
+
+def _cgroup_cpus():
+    """CPUs of this process's cgroup v2 quota (cpu.max "quota period"), or None if unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        return None
 
 
 def _physical_cores():

@@ -68,7 +68,8 @@ class TorchCpuLlama:
     """The map call on the CPU, over the engine's own synthetic weights (ms_init_synthetic /
     oracle/synth.py: same seed, std, norm jitter -> the same bf16 values)."""
 
-    def __init__(self, cfg, seed: int = 0, std: float = 0.02, jitter: float = 0.0, dtype=torch.bfloat16):
+    def __init__(self, cfg, seed: int = 0, std: float = 0.02, jitter: float = 0.0, dtype=torch.bfloat16,
+                 progress=None):
         self.cfg, self.dt = cfg, dtype
         H, D, F_ = cfg.hidden, cfg.head_dim, cfg.ffn
         QD, KD = cfg.n_heads * D, cfg.n_kv_heads * D
@@ -85,6 +86,8 @@ class TorchCpuLlama:
                 "wgu": torch.cat([lin(S.WGATE, l, F_, H), lin(S.WUP, l, F_, H)]), "wdown": lin(S.WDOWN, l, H, F_),
                 "n1": synth_norm(seed, S.ATTN_NORM, l, H, jitter, dtype),
                 "n2": synth_norm(seed, S.FFN_NORM, l, H, jitter, dtype)})
+            if progress is not None and (l + 1) % 4 == 0:
+                progress(f"weights: {l + 1}/{cfg.n_layers} layers")
         self.final_norm = synth_norm(seed, S.FINAL_NORM, 0, H, jitter, dtype)
         self.inv_freq = torch.tensor(rope_inv_freq(cfg), dtype=torch.float64)
 
@@ -160,7 +163,8 @@ def time_chunk(cfg, prompt_ids, gen_len: int, decode_sample: int = 16, seed: int
     def note(msg):  # progress on stderr: a GPU-box run that prints nothing for minutes looks hung
         print(f"[cpu_baseline] {msg}", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    m = TorchCpuLlama(cfg, seed=seed, std=std)
+    note(f"building weights ({torch.get_num_threads()} threads)")
+    m = TorchCpuLlama(cfg, seed=seed, std=std, progress=note)
     note(f"weights built in {time.perf_counter() - t0:.1f} s, {torch.get_num_threads()} threads")
     ids = torch.as_tensor(prompt_ids, dtype=torch.long)
     P = ids.shape[0]
