@@ -124,10 +124,10 @@ class TorchCpuLlama:
             v = qkv[:, (Hq + Hk) * D:].view(T, Hk, D)
             kc, vc = cache[l]
             kc[p0:p0 + T], vc[p0:p0 + T] = k, v
-            K = kc[:p0 + T].transpose(0, 1).repeat_interleave(Hq // Hk, 0)
-            V = vc[:p0 + T].transpose(0, 1).repeat_interleave(Hq // Hk, 0)
+            K = kc[:p0 + T].transpose(0, 1)  # [Hk][keys][D]: grouped-query SDPA reads each kv
+            V = vc[:p0 + T].transpose(0, 1)  # head for its Hq / Hk query heads (no repeat copy)
             o = F.scaled_dot_product_attention(q.transpose(0, 1), K, V, is_causal=(T > 1 and p0 == 0),
-                                               scale=1.0 / math.sqrt(D))
+                                               scale=1.0 / math.sqrt(D), enable_gqa=True)
             x = x + (o.transpose(0, 1).reshape(T, Hq * D) @ L["wo"].T).float()
             gu = self._proj(x, L["n2"], L["wgu"])
             h = F.silu(gu[:, :cfg.ffn].float()) * gu[:, cfg.ffn:].float()

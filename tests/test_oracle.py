@@ -109,3 +109,9 @@ def test_torch_cpu_baseline_is_the_same_model():
     ref, _ = o.forward(ids)
     got = m.last_logits.numpy()
     assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 3e-2
+    # the decode path (one new token over the grouped-query KV cache) continues the prefill
+    cache = m.new_cache(96)
+    m.forward(torch.as_tensor(ids[:-1]), cache, 0)
+    m.forward(torch.as_tensor(ids[-1:]), cache, len(ids) - 1)
+    dec = m.last_logits.numpy()
+    assert np.linalg.norm(dec - got) / np.linalg.norm(got) < 3e-2
