@@ -140,6 +140,17 @@ struct ms_engine {
   // tiles measured no faster than split-K 4 + residual_rmsnorm, 1.962 vs 1.955 ms per Q4_K_M
   // decode step, profiles/r03/v7_q4_resid_fused_rejected.txt).
   bool resid_fuse = true, has_quant = false;
+  // the layer's decode MLP as one launch (k_mlp.hip: gate/up, a chip-wide hand-off of h, down
+  // + residual; bit-identical to the two launches), engines of <= 8 slots on fp16 MLP weights:
+  // opt-in (MS_MLP_FUSED=1) -- measured no faster than the two launches, 2.158 vs 2.130 ms per
+  // decode step at B = 8 (profiles/r04/v13_*).  mlp_sync_d: [0..1] counters, [16] timeout flag
+  bool mlp_fuse = false, mlp_used = false;
+  unsigned* mlp_sync_d = nullptr;
+  unsigned* mlp_err_h = nullptr;
+  bool mlp_fused(const QSlot* gu, const QSlot* dn, int B) const {
+    return mlp_fuse && resid_fused(gu) && resid_fused(dn) && cfg.max_batch <= 8 &&
+           mlp_decode_supported(B, H, F, H / resid_rt);
+  }
   int resid_rt = 12;
   bool resid_fused(const QSlot* q) const {
     return resid_fuse && !large_engine && !(q && q->ready());
@@ -451,6 +462,19 @@ struct ms_engine {
     prof_end(K_ATTN_DECODE);
     resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm);
     const RowScale rs_ffn = cur_rs;
+    const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
+    if (mlp_fused(&Q[QS_GU], &Q[QS_DOWN], B)) {
+      // xb / ssq are the gate/up input AND the down epilogue's outputs: every workgroup has
+      // consumed them before the hand-off that precedes the first write
+      prof_begin(K_GEMV);
+      launch_mlp_decode(xb, Ly.wgu, Ly.wdown, hbuf, x, B, H, F, rs_ffn, ssq, g_next, xb, mlp_sync_d,
+                        mlp_sync_d + 16, stream);
+      prof_end(K_GEMV);
+      mlp_used = true;
+      pending_split = 0;
+      cur_rs = make_row_scale(ssq, H / resid_rt, H, cfg.norm_eps);
+      return;
+    }
     if (large(B)) {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
@@ -462,7 +486,6 @@ struct ms_engine {
       gg.rs = rs_ffn;
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV, sizeof(f16_t));
     }
-    const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
     resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next);
   }
 
@@ -484,7 +507,8 @@ struct ms_engine {
     // profiles/r04/v5_prefill_fusions_prof_*.txt)
     gemm_or_gemv(xb, Ly.wqkv, qkv, T, QKVN, H, QKVN, MS_EPI_STORE_F16, decode, kc, &rs_attn);
     prof_begin(K_MISC);
-    launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream);
+    // prefill: K / V only -- the attention kernel rotates Q while staging it (pa.cos_tab)
+    launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream, decode || !pa.cos_tab);
     prof_end(K_MISC);
     if (decode) {
       prof_begin(K_ATTN_DECODE);
@@ -755,6 +779,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
+    if (const char* v = getenv("MS_MLP_FUSED")) E.mlp_fuse = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
     // the consumers stage the 256-tile statistics in LDS: engines of <= 16 slots (per engine,
@@ -771,6 +796,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * 256 * sizeof(int32_t),
                          hipHostMallocDefault));
     E.ids_ring_d = E.dalloc<int32_t>((size_t)ms_engine::kMaxRun * 256);
+    E.mlp_sync_d = E.dalloc<unsigned>(64, true);
+    HIP_OK(hipHostMalloc((void**)&E.mlp_err_h, 64, hipHostMallocDefault));
+    *E.mlp_err_h = 0;
     HIP_OK(hipHostMalloc((void**)&E.first_host, (size_t)cfg->max_batch * sizeof(int32_t), hipHostMallocDefault));
     if (const char* v = getenv("MS_DECODE_RUN")) E.max_run = std::max(1, std::min(atoi(v), (int)ms_engine::kMaxRun));
     if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
@@ -794,6 +822,7 @@ int ms_destroy(ms_engine* e) {
   for (ms_engine::Ctx* c : {&e->cp, &e->cd})
     if (c->args_h) (void)hipHostFree(c->args_h);
   if (e->ids_host) (void)hipHostFree(e->ids_host);
+  if (e->mlp_err_h) (void)hipHostFree(e->mlp_err_h);
   if (e->first_host) (void)hipHostFree(e->first_host);
   if (e->bt_h) (void)hipHostFree(e->bt_h);
   for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
@@ -1247,6 +1276,8 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   pa.seq_slot = d + o_sslot;
   pa.qblk = d + o_qblk;
   pa.n_qblk = (int)qb.size();
+  pa.cos_tab = E.cos_tab;  // Q is rotated by the attention kernel as it stages it
+  pa.sin_tab = E.sin_tab;
   DecodeAttnArgs da{};
 
   E.prof_begin(K_MISC);
@@ -1377,8 +1408,15 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
   HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_ring_d, (size_t)k * B * sizeof(int32_t), hipMemcpyDeviceToHost,
                         E.stream));
+  if (E.mlp_used)
+    HIP_OK(hipMemcpyAsync(E.mlp_err_h, E.mlp_sync_d + 16, sizeof(unsigned), hipMemcpyDeviceToHost, E.stream));
   ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
+  if (E.mlp_used && *E.mlp_err_h) {  // a workgroup of the fused MLP was not resident: never silent
+    E.mlp_fuse = false;
+    REQUIRE(false, MS_EIO, "fused decode MLP: hand-off timed out (not every workgroup resident); "
+                           "fusion disabled for this engine, the step's ids are invalid");
+  }
   std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));
 }
 

@@ -118,12 +118,53 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   char* qimg = smem + 2 * 32768;
   const int qrow_l = wave * 16 + r;
   {
-    const f16_t* qrow = qkv + (size_t)(qstart + min(qi, qlen - 1)) * row_stride + h0 * kHeadDim;
+    const int qr = min(qi, qlen - 1);
+    const f16_t* qrow = qkv + (size_t)(qstart + qr) * row_stride + h0 * kHeadDim;
+    if (a.cos_tab) {
+      // Q straight from the GEMM: head dims in the rope-permuted order (the 16-element group
+      // g8 holds dims 8 g8 .. +7, then 64 + 8 g8 .. +7), rotated here with rope_kv_kernel's
+      // arithmetic (fp16 in, fp32 rotation, fp16 out) into natural chunks g8 and 8 + g8 --
+      // which are this lane group's chunks 4s + g for s = t and 2 + t (g8 = 4t + g)
+      const int pos = kvlen - qlen + qr;
+      const float* ct = a.cos_tab + (size_t)pos * 64;
+      const float* st = a.sin_tab + (size_t)pos * 64;
 #pragma unroll
-    for (int hh = 0; hh < GB; ++hh)
+      for (int t = 0; t < 2; ++t) {
+        const int g8 = 4 * t + g;
+        const float4 c0 = *(const float4*)(ct + 8 * g8), c1 = *(const float4*)(ct + 8 * g8 + 4);
+        const float4 s0 = *(const float4*)(st + 8 * g8), s1 = *(const float4*)(st + 8 * g8 + 4);
+        const float cc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float ss[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
+        for (int hh = 0; hh < GB; ++hh) {
+          const uint4 lo = *(const uint4*)(qrow + hh * kHeadDim + 16 * g8);
+          const uint4 hi = *(const uint4*)(qrow + hh * kHeadDim + 16 * g8 + 8);
+          const uint32_t lw[4] = {lo.x, lo.y, lo.z, lo.w}, hw[4] = {hi.x, hi.y, hi.z, hi.w};
+          uint32_t ra[4], rb[4];
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            float r0[2], r1[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const float av = e ? h_hi(lw[p]) : h_lo(lw[p]), bv = e ? h_hi(hw[p]) : h_lo(hw[p]);
+              const float c = cc[2 * p + e], sn = ss[2 * p + e];
+              r0[e] = __fsub_rn(__fmul_rn(av, c), __fmul_rn(bv, sn));
+              r1[e] = __fadd_rn(__fmul_rn(bv, c), __fmul_rn(av, sn));
+            }
+            ra[p] = pack2h(r0[0], r0[1]);
+            rb[p] = pack2h(r1[0], r1[1]);
+          }
+          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * t + g)) = uint4{ra[0], ra[1], ra[2], ra[3]};
+          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * (2 + t) + g)) = uint4{rb[0], rb[1], rb[2], rb[3]};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int hh = 0; hh < GB; ++hh)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
+    }
   }
   f32x4 o[GB][8];
   float m_run[GB], l_run[GB];

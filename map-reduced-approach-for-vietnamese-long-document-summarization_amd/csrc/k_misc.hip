@@ -235,7 +235,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(f16_t* __restrict__ qkv, i
                                                       const int32_t* __restrict__ tok_slot,
                                                       const float* __restrict__ cos_tab,
                                                       const float* __restrict__ sin_tab,
-                                                      KVView kv) {
+                                                      KVView kv, int h_begin) {
   __shared__ __attribute__((aligned(16))) f16_t st[64 * kHeadDim];  // <= 64 Q+K heads
   const int t = blockIdx.x;
   const int pos = tok_pos[t];
@@ -244,13 +244,14 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(f16_t* __restrict__ qkv, i
   const int off = pos % kPage;
   const int row_elems = (Hq + 2 * Hk) * kHeadDim;
   f16_t* row = qkv + (size_t)t * row_elems;
-  const int qk_elems = (Hq + Hk) * kHeadDim;
-  for (int c = threadIdx.x; c < qk_elems / 8; c += blockDim.x)
-    *(uint4*)(st + c * 8) = *(const uint4*)(row + c * 8);
+  // heads h_begin.. (0: Q, K and V; Hq: K and V only)
+  const int qk_elems = (Hq + Hk) * kHeadDim, e0 = h_begin * kHeadDim;
+  for (int c = threadIdx.x; c < (qk_elems - e0) / 8; c += blockDim.x)
+    *(uint4*)(st + e0 + c * 8) = *(const uint4*)(row + e0 + c * 8);
   __syncthreads();
-  const int items = (Hq + 2 * Hk) * 16;
+  const int items = (Hq + 2 * Hk - h_begin) * 16;
   for (int it = threadIdx.x; it < items; it += blockDim.x) {
-    const int head = it >> 4;
+    const int head = h_begin + (it >> 4);
     const int i0 = (it & 15) * 4;  // dims i0..i0+3 and 64+i0..64+i0+3
     uint2 olo, ohi;
     if (head < Hq + Hk) {  // Q or K: rotate (from the permuted staging copy)
@@ -295,10 +296,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(f16_t* __restrict__ qkv, i
 
 void launch_rope_kv(f16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
-                    KVView kv, hipStream_t s) {
+                    KVView kv, hipStream_t s, bool rope_q) {
   if (T <= 0) return;
   MS_LAUNCH(rope_kv_kernel, dim3(T), dim3(256), 0, s, qkv, Hq, Hk, tok_pos, tok_slot,
-                     cos_tab, sin_tab, kv);
+                     cos_tab, sin_tab, kv, rope_q ? 0 : Hq);
 }
 
 // ---------------------------------------------------------------- greedy argmax

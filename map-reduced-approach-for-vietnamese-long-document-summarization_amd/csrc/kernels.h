@@ -25,6 +25,10 @@ struct PrefillAttnArgs {
   const int32_t* seq_slot;    // [S] block-table row
   const int32_t* qblk;        // [NQB] (seq << 16) | q_block (kPrefillQRows rows), heaviest first
   int32_t n_qblk;
+  // non-null: Q arrives straight from the QKV GEMM (rope-permuted, not rotated) and the kernel
+  // applies RoPE while staging it (rope_kv_kernel's arithmetic); null: Q already rotated
+  const float* cos_tab;
+  const float* sin_tab;
 };
 
 struct DecodeAttnArgs {
@@ -73,9 +77,10 @@ void launch_rmsnorm(const float* x, const f16_t* w, f16_t* y, float* ssq, int ro
                     const int32_t* row_idx, hipStream_t s);
 // RoPE on Q (in place, rope-permuted -> natural dim order) and K; K,V scattered into the
 // paged cache.  Q/K heads arrive in the rope-permuted row order of the fused weights.
+// rope_q = false: K and V only (prefill: the attention kernel rotates Q as it stages it)
 void launch_rope_kv(f16_t* qkv, int T, int Hq, int Hk, const int32_t* tok_pos,
                     const int32_t* tok_slot, const float* cos_tab, const float* sin_tab,
-                    KVView kv, hipStream_t s);
+                    KVView kv, hipStream_t s, bool rope_q = true);
 void launch_argmax(const float* logits, int rows, int n, int32_t* out, hipStream_t s);
 
 // out (epi) A[M][K] . W[N][K]^T, MFMA 16x16x32 fp16, K % 64 == 0; rs (<= kGemmRsTiles tiles of
@@ -139,6 +144,14 @@ struct GemvArgs {
   // writes its rows into the batch's [S][B][N] slabs (slab_rows = B, out = slab 0, row r0)
   int slab_rows;
 };
+// the decode MLP of one layer as one launch (k_mlp.hip): h = SwiGLU(rs . xb Wgu^T) [M][F], then
+// x += h Wdown^T with the RESID_SSQ epilogue on 12-row tiles (ssq_out [256][M], xg_out =
+// f16(x * gamma_next)); bit-identical to the two GEMV launches.  sync: 2 zeroed counters the
+// kernel leaves zeroed; err: set on a hand-off timeout.  M <= 8, H = 3072, F = 8192.
+bool mlp_decode_supported(int M, int H, int F, int rs_tiles);
+void launch_mlp_decode(const f16_t* xb, const f16_t* wgu, const f16_t* wdown, f16_t* h, float* x, int M, int H,
+                       int F, const RowScale& rs, float* ssq_out, const f16_t* gamma_next, f16_t* xg_out,
+                       unsigned* sync, unsigned* err, hipStream_t s);
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)
 bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);

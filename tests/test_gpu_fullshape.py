@@ -420,6 +420,24 @@ def test_config2_continuous_batching_full_width(oracle):
         e.close()
 
 
+def test_fused_decode_mlp_bit_exact(dev, chunks, monkeypatch):
+    """The one-launch decode MLP (k_mlp.hip: gate/up, a chip-wide hand-off of h, down + the
+    residual epilogue) against the two GEMV launches it replaces: identical greedy ids at the
+    benchmarked widths (8 slots: the fused engine; the hand-off runs once per layer per decode
+    step; the kernel restates the two launches' arithmetic exactly)."""
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MS_MLP_FUSED", fused)
+        e = Engine(CFG, device=0, max_batch=NCHUNK, max_ctx=P + 64, max_prefill_tokens=NCHUNK * P)
+        try:
+            e.init_synthetic(SEED, STD, JIT)
+            res = e.generate(list(chunks), num_predict=48, ignore_eos=True)
+            outs.append([r.ids for r in res])
+        finally:
+            e.close()
+    assert outs[0] == outs[1]
+
+
 def test_prefill_packing_invariance(dev):
     """A prompt's prefill does not depend on what it is packed with: alone (600 rows: the
     128x128 GEMM tile) and behind a 1500-token prompt (2100 rows: the 256x256 tile) its hidden
