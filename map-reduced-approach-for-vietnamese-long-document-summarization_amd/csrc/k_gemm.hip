@@ -157,6 +157,23 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
   // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
   gemm_rs_dma<GBM, 4>(rs, M, m0, rinv_s, rs_stage);
+  // residual epilogue: x as the accumulators' initial value (as gemm256_kernel)
+  f16_t g4[4] = {0, 0, 0, 0};  // raw bits, converted in the epilogue
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = min(m0 + wm * 64 + m * 16 + fg * 4 + j, M - 1);
+          const int col = min(n0 + wn * 64 + n * 16 + fr, N - 1);
+          acc[m][n][j] = ((const float*)out)[(size_t)row * ldo + col];
+        }
+    const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;  // unconditional load (no merge wait)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) g4[n] = gp[min(n0 + wn * 64 + n * 16 + fr, N - 1)];
+  }
   stage(0, 0);
   wait_vmcnt0();
   __syncthreads();
@@ -190,42 +207,23 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
   }
 
   // epilogue: acc[m][n][j] = C[row 4*fg + j][col fr] of 16x16 tile (m, n)
-  if constexpr (EPI == 1) {  // residual add: 32 loads in flight, then the adds and stores
+  if constexpr (EPI == 1) {  // residual add (x was the accumulators' initial value)
     const bool fuse = gr.xg != nullptr;
-    float g4[4] = {0.f, 0.f, 0.f, 0.f};
     float ss[4][4] = {};
-    if (fuse)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) g4[n] = h2f(gr.gamma[min(n0 + wn * 64 + n * 16 + fr, N - 1)]);
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int m0_ = 0; m0_ < 4; m0_ += 2) {
-      float r[2][4][4];
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            const int row = min(m0 + wm * 64 + (m0_ + h) * 16 + fg * 4 + j, M - 1);
-            const int col = min(n0 + wn * 64 + n * 16 + fr, N - 1);
-            r[h][j][n] = __builtin_nontemporal_load(((const float*)out) + (size_t)row * ldo + col);
+        for (int n = 0; n < 4; ++n) {
+          const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
+          const int col = n0 + wn * 64 + n * 16 + fr;
+          const float v = acc[m][n][j];
+          if (row < M && col < N) {
+            ((float*)out)[(size_t)row * ldo + col] = v;
+            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g4[n]), ss[m][j]);
           }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int n = 0; n < 4; ++n) {
-            const int row = m0 + wm * 64 + (m0_ + h) * 16 + fg * 4 + j;
-            const int col = n0 + wn * 64 + n * 16 + fr;
-            const float v = r[h][j][n] + acc[m0_ + h][n][j];
-            if (row < M && col < N) {
-              ((float*)out)[(size_t)row * ldo + col] = v;
-              if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, g4[n], ss[m0_ + h][j]);
-            }
-          }
-    }
+        }
     if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, N, m0, n0, gr);
     return;
   }
@@ -399,17 +397,39 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   // the rows' sums of squares by LDS DMA ahead of the first tile (no register: a register
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
   gemm_rs_dma<TBM, 8>(rs, M, m0, rinv_s, rs_stage);
+  // residual epilogue: the tile's x is the accumulators' initial value, loaded ahead of the
+  // first K tile (the prologue's vmcnt waits retire it with tile 0), so the MFMAs add A . W^T
+  // onto x and the epilogue only stores -- no load round trips after the K loop
+  f16_t g4[4] = {0, 0, 0, 0};  // raw bits: converted in the epilogue (a conversion here waited)
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = min(m0 + wr * 128 + mi * 16 + fg * 4 + j, M - 1);
+          const int col = min(n0 + wc * 64 + ni * 16 + fr, N - 1);
+          acc[mi][ni][j] = ((const float*)out)[(size_t)row * ldo + col];
+        }
+    // unconditional (a conditional load's merge made the wave wait for it right here)
+    const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) g4[ni] = gp[min(n0 + wc * 64 + ni * 16 + fr, N - 1)];
+  }
   // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
   stage(0, 0, 0);
   stage(0, 3, 0);
   stage(0, 1, 0);
   stage(0, 2, 0);
+  // (compiler-visible waits: they also retire the residual epilogue's x loads, issued first,
+  // so no extra vmcnt(0) is inserted ahead of the K loop for the accumulators)
   if (nk > 1) {
     stage(1, 0, TBK);
     stage(1, 3, TBK);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((4 & 0xF) | (0x7 << 4) | (0xF << 8));  // vmcnt(4)
   } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));  // vmcnt(0)
   }
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the two wave rows by one barrier
@@ -445,47 +465,24 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
 
   // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x64
   if constexpr (EPI == 1) {
-    // residual add: the 32 fp32 loads of two 16-row groups are issued together before their
-    // adds and stores (a plain `out[o] += acc` compiled to 128 dependent load -> wait ->
-    // store round trips per lane); with gr.xg also the next projection's input and statistics
+    // residual add (x was the accumulators' initial value): store x, and with gr.xg also the
+    // next projection's input and its statistics
     const bool fuse = gr.xg != nullptr;
-    float g4[4] = {0.f, 0.f, 0.f, 0.f};
     float ss[8][4] = {};
-    if (fuse)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) g4[ni] = h2f(gr.gamma[min(n0 + wc * 64 + ni * 16 + fr, N - 1)]);
+    for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-    for (int mi0 = 0; mi0 < 8; mi0 += 2) {
-      float r[2][4][4];
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            // clamped rows/cols: every load is in bounds and unconditional (one basic block)
-            const int row = min(m0 + wr * 128 + (mi0 + h) * 16 + fg * 4 + j, M - 1);
-            const int col = min(n0 + wc * 64 + ni * 16 + fr, N - 1);
-            r[h][j][ni] = __builtin_nontemporal_load(((const float*)out) + (size_t)row * ldo + col);
+        for (int ni = 0; ni < 4; ++ni) {
+          const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
+          const int col = n0 + wc * 64 + ni * 16 + fr;
+          const float v = acc[mi][ni][j];
+          if (row < M && col < N) {
+            ((float*)out)[(size_t)row * ldo + col] = v;
+            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g4[ni]), ss[mi][j]);
           }
-      // keep the batch: under 216 live VGPRs the scheduler would otherwise sink every load
-      // next to its store (one round trip per element)
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) {
-            const int row = m0 + wr * 128 + (mi0 + h) * 16 + fg * 4 + j;
-            const int col = n0 + wc * 64 + ni * 16 + fr;
-            const float v = r[h][j][ni] + acc[mi0 + h][ni][j];
-            if (row < M && col < N) {
-              ((float*)out)[(size_t)row * ldo + col] = v;
-              if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, g4[ni], ss[mi0 + h][j]);
-            }
-          }
-    }
+        }
     if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, N, m0, n0, gr);
     return;
   }
