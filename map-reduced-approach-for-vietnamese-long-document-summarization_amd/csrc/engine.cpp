@@ -1694,6 +1694,12 @@ int ms_set_gemm_variant(int32_t v) {
   return MS_OK;
 }
 
+int ms_set_qgemv_gs(int32_t on) {
+  if (on < 0 || on > 1) return MS_EINVAL;
+  set_qgemv_gs(on != 0);
+  return MS_OK;
+}
+
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K) {
   if (M < 1 || M > 64 || N < 16 || K < 64 || K % 64) return MS_EINVAL;
   return (int64_t)gemv_workspace_bytes(M, N, K);

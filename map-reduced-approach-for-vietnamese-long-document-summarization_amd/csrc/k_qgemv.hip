@@ -28,6 +28,7 @@
 //     exact fp32 dequantised weights (no fp16 rounding of them, and no cancellation: a
 //     1024 + q bias form cost ~7e-6 relative against fp64);
 //   * Q6_K, dequantised in registers to the fp16 values of the fp16 copy.
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemv_common.h"
@@ -359,6 +360,123 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
   gemv_finish<MT, NT, EPI, RS>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, ResidPre{0.f, 0.f}, rsd);
 }
 
+// ---- the Q6_K lm_head (greedy argmax partials) as a grid-stride two-stage loop.  One-tile
+// blocks (qgemv_kernel) each DMA the whole X image (M x K fp16: 48 KiB at M = 8 -- 385 MB over
+// the vocabulary's 8016 tiles, more than the weights' 323 MB) and pay one exposed weight
+// latency per tile.  Here 2 x 256 resident blocks stage X and the rows' norm factors once,
+// then walk tiles b, b + G, ...: each wave issues the NEXT tile's weight loads (17 VGPRs)
+// before it dequantises and multiplies the current one, and the per-tile cross-wave reduction
+// uses LDS-only barriers so those loads stay in flight.  Per tile the arithmetic is
+// qgemv_kernel<1, 1, ARGMAX, 1, LDS, true>'s exactly (same K split over waves, same MFMA order,
+// same reduction order and epilogue): bit-identical partials.
+struct Q6Regs {
+  uint4 qa, qb, qh, sc;
+  uint32_t dw;
+};
+__device__ __forceinline__ void q6_fetch(Q6Regs& r, const uint8_t* base, int row_bytes, int n0, int fr, int sb,
+                                         int hh, int p) {
+  const uint8_t* bp = base + (size_t)(n0 + fr) * row_bytes + (size_t)sb * kQ6KPacked;
+  r.qa = ldw16(bp + hh * 64 + 16 * p);
+  r.qb = ldw16(bp + hh * 64 + 32 + 16 * p);
+  r.qh = ldw16(bp + 128 + hh * 32 + 16 * p);
+  r.sc = ldw16(bp + 192);
+  r.dw = *(const uint32_t*)(bp + 208);
+}
+__global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(6, 8))) void qgemv_q6_argmax_gs_kernel(const f16_t* __restrict__ X, QMat qm,
+                                                                float2* __restrict__ out, int M, int N, int K,
+                                                                int ldo, int red_off, int rinv_off, GemvArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ELEMS = 256;  // MT = NT = 1
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, g = lane >> 4, hh = g >> 1, p = g & 1;
+  const int tiles = N / 16, G = gridDim.x;
+  const uint8_t* base = qm.base0;
+  const int row_bytes = qm.row_bytes0;
+  // 0. row statistics and X once per block, then the first tile's weights
+  const bool rs_on = ga.rs.ssq != nullptr;
+  if (rs_on) rs_begin<false>(smem, rinv_off, ga.rs, M);
+  gemv_dma_x(smem, X, M, K, K);
+  __builtin_amdgcn_sched_barrier(0);
+  Q6Regs cur, nxt;
+  int t = blockIdx.x;
+  q6_fetch(cur, base, row_bytes, t * 16, fr, wave, hh, p);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));  // X and the statistics landed (issued first)
+  __builtin_amdgcn_s_barrier();
+  float* rinv = (float*)(smem + rinv_off);
+  if (rs_on) rs_finish<false>(smem, rinv_off, ga.rs, M, 0.f);
+  lds_sync();
+  float* red = (float*)(smem + red_off);
+  for (; t < tiles; t += G) {
+    const bool more = t + G < tiles;
+    if (more) q6_fetch(nxt, base, row_bytes, (t + G) * 16, fr, wave, hh, p);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) __builtin_amdgcn_s_waitcnt(vmcnt_imm(5));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    // qgemv_kernel's Q6_K body, SBW = 1 (this wave's super-block = its index), MT = NT = 1
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    const float d = h2f_lo(cur.dw);
+#pragma unroll
+    for (int tt = 0; tt < 8; ++tt) {
+      const int k4 = tt >> 1, sub = tt & 1;
+      const int si = hh * 8 + p + 2 * k4;
+      const float ds = __fmul_rn(d, (float)(int)(int8_t)byte_of(cur.sc, si));
+      const float nds = -32.0f * ds;
+      const uint4 qsrc = (k4 & 1) ? cur.qb : cur.qa;
+      uint32_t pk[4];
+#pragma unroll
+      for (int w = 0; w < 2; ++w) {
+        const int wi = 2 * sub + w;
+        const uint32_t aw = wi == 0 ? qsrc.x : wi == 1 ? qsrc.y : wi == 2 ? qsrc.z : qsrc.w;
+        const uint32_t hw = wi == 0 ? cur.qh.x : wi == 1 ? cur.qh.y : wi == 2 ? cur.qh.z : cur.qh.w;
+        const uint32_t q4 = (((k4 >> 1) ? (aw >> 4) : aw) & 0x0F0F0F0Fu) | (((hw >> (2 * k4)) & 0x03030303u) << 4);
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        const f2 ds2 = {ds, ds}, nds2 = {nds, nds};
+        const f2 y01 = __builtin_elementwise_fma(ds2, f2{(float)(q4 & 0xFFu), (float)((q4 >> 8) & 0xFFu)}, nds2);
+        const f2 y23 = __builtin_elementwise_fma(ds2, f2{(float)((q4 >> 16) & 0xFFu), (float)(q4 >> 24)}, nds2);
+        pk[2 * w] = pack2h(y01.x, y01.y);
+        pk[2 * w + 1] = pack2h(y23.x, y23.y);
+      }
+      const f16x8 wf = __builtin_bit_cast(f16x8, pk);
+      const int k = wave * 256 + hh * 128 + k4 * 32 + 16 * p + 8 * sub;
+      const int xrow = min(fr, M - 1);
+      acc = mfma16(*(const f16x8*)(smem + x_lds(xrow, k, K)), wf, acc);
+    }
+    // cross-wave reduction (LDS-only barriers: the next tile's loads stay in flight)
+    *(f32x4*)&red[wave * ELEMS + lane * 4] = acc;
+    lds_sync();
+    if ((int)threadIdx.x < ELEMS) {
+      const int e = threadIdx.x, l = (e >> 2) & 63, j = e & 3;
+      const int row = 4 * (l >> 4) + j, col = t * 16 + (l & 15);
+      float v = -INFINITY;
+      if (row < M && col < N) {
+        float sum = 0.f;
+        for (int q = 0; q < nw; ++q) sum += red[q * ELEMS + e];
+        v = sum * (rs_on ? rinv[row] : 1.0f);
+      }
+      if (!(v == v)) v = -INFINITY;
+      int idx = col;
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+      if ((l & 15) == 0 && row < M) out[(size_t)row * ldo + t] = make_float2(v, __int_as_float(idx));
+    }
+    lds_sync();  // red is rewritten by the next tile
+    cur = nxt;
+  }
+}
+
+// whether the Q6_K lm_head takes the grid-stride form (MS_QGEMV_GS=0 / ms_set_qgemv_gs(0):
+// one-tile blocks)
+static int g_q6_gs = -1;
+void set_qgemv_gs(bool on) { g_q6_gs = on ? 1 : 0; }
+static bool q6_gs_on() {
+  if (g_q6_gs < 0) {
+    const char* e = getenv("MS_QGEMV_GS");
+    g_q6_gs = (!e || atoi(e) != 0) ? 1 : 0;
+  }
+  return g_q6_gs != 0;
+}
+
 struct QPlan {
   int MT, NT, SBW, waves, tiles;
 };
@@ -464,6 +582,21 @@ void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K,
   if (p.waves == 0) return;  // callers check qgemv_supported()
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
+  if (epi == MS_GEMV_EPI_ARGMAX && q6_gs_on() && q.n == 1 && q.type0 == MS_QT_Q6_K && p.MT == 1 && p.SBW == 1 &&
+      N % 16 == 0) {
+    ga.rs = RowScale{};  // as qgemv_go: a row's positive scale never moves its argmax
+    // LDS: [X image][per-wave partials][rinv][staged statistics]
+    const int red_off = (int)((gemv_x_lds_bytes(M, K) + 15) / 16 * 16);
+    const size_t main_bytes = (size_t)red_off + (size_t)p.waves * 256 * 4;
+    const int ro = (int)gemv_rinv_offset(main_bytes);
+    const size_t lds = gemv_lds_total(main_bytes, ga.rs, M);
+    if (lds <= kLdsCap) {
+      const int grid = std::min(N / 16, 512);  // two resident blocks per CU
+      MS_LAUNCH(qgemv_q6_argmax_gs_kernel, dim3(grid), dim3(64 * p.waves), lds, s, X, q, (float2*)out, M, N, K, ldo,
+                red_off, ro, ga);
+      return;
+    }
+  }
   switch (p.MT) {
     case 1: qgemv_go_mt<1>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;
     case 2: qgemv_go_mt<2>(X, q, out, M, N, K, ldo, epi, p, ga, s); break;

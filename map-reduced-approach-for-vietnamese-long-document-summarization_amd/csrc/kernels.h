@@ -104,6 +104,8 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
                  int epi, hipStream_t s, const RowScale* rs = nullptr, const GemmResid* gr = nullptr);
 // tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
 void set_gemm_variant(int v);
+// the Q6_K lm_head argmax GEMV: grid-stride two-stage loop (default) or one-tile blocks
+void set_qgemv_gs(bool on);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {

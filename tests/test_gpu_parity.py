@@ -844,6 +844,35 @@ def test_qgemv_argmax_vs_fp64(lib, dev, qtype, M, N, K):
             assert int(got[r]) == int(torch.argmax(ref[r])), r
 
 
+@pytest.mark.parametrize("M,N,rs", [(8, 32768, True), (1, 4096, False), (16, 8192, True), (5, 1040, True)])
+def test_q6_lm_head_grid_stride_bit_exact(lib, dev, M, N, rs):
+    """The grid-stride two-stage Q6_K lm_head (k_qgemv.hip qgemv_q6_argmax_gs_kernel) writes the
+    same {max, id} partials, bit for bit, as the one-tile blocks -- with and without the rows'
+    deferred-norm scale, at the vocabulary's width and at ragged tile counts."""
+    K = 3072
+    b, wbf, pk = _packed(lib, dev, Q.GGML_TYPE_Q6_K, N, K, 11 + M)
+    g = torch.Generator(device="cpu").manual_seed(N + M)
+    X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
+    ssq = (torch.rand(M, generator=g) * K + 1.0).to(dev)
+    outs = []
+    for gs in (1, 0):
+        L.check(lib.ms_set_qgemv_gs(gs))
+        part = torch.full((M, N // 16, 2), float("nan"), device=dev)
+        if rs:
+            L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), 1, K, 1e-5))
+        try:
+            L.check(lib.ms_op_qgemv(X.data_ptr(), Q.GGML_TYPE_Q6_K, pk.data_ptr(), part.data_ptr(), M, N, K, N // 16,
+                                    L.MS_EPI_ARGMAX, _stream()))
+        finally:
+            if rs:
+                L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
+        torch.cuda.synchronize()
+        outs.append(part.cpu())
+    L.check(lib.ms_set_qgemv_gs(1))
+    assert not torch.isnan(outs[0]).any()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+
+
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("N,K,S", [(256, 3072, 6), (512, 3072, 4), (128, 8192, 4), (256, 8192, 2),
