@@ -72,6 +72,16 @@ __device__ __forceinline__ float grp_sum(float x) {
 // step, profiles/r01 v5_nt_stream_ab_rejected)
 __device__ __forceinline__ u32x4 ld_stream(const f16_t* p) { return *(const u32x4*)p; }
 
+// One 16-B-per-lane LDS DMA (1 KiB per wave at lds + 16 * lane), issued where the compiler
+// cannot see it: after a visible global_load_lds the compiler waits vmcnt(0) before every
+// ds_read_b64_tr_b16 (it cannot prove the transposed V reads miss the DMA's LDS bytes), so the
+// prefill's P.V of tile t waited for tile t+1's DMA to land.  Callers order the DMA themselves
+// (s_waitcnt vmcnt(0) + barrier before the buffer is read).
+__device__ __forceinline__ void dma16_opaque(const void* src, const char* lds) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS_AS const char*)lds);
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"{m0}"(m0), "v"(src) : "memory");
+}
+
 // ============================================================ prefill (varlen, causal)
 // 1-D grid over (q-block, head group), heaviest q-blocks first for every head group; block
 // 512 = 8 waves x 16 query rows (kPrefillQRows = 128), GB q heads of ONE kv head (GQA group, or
@@ -183,33 +193,42 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
 
   // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
   // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
-  auto dma_tile = [&](int t, int buf) {
-    const int pid = kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t];
-    const size_t base = ((size_t)pid * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+  auto page_of = [&](int t) { return kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t]; };
+  // (waves 0-3 load K, 4-7 V: J >> 4 = wave >> 2; the source array is picked once, in scalar
+  // registers -- a per-piece select reloaded the kernel argument by a vector load every tile)
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const bool dma_v = wave_u >= 4;
+  const f16_t* dma_src = dma_v ? kv.v : kv.k;
+  const int n_kv_heads = kv.n_kv_heads;
+  auto dma_tile = [&](int pid, int t, int buf) {
+    const f16_t* page = dma_src + ((size_t)pid * n_kv_heads + kvh) * kPage * kHeadDim;
     const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
-    char* img = smem + buf * 32768;
+    char* img = smem + buf * 32768 + (dma_v ? 16384 : 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int J = 4 * wave + i, isv = J >> 4;
+      const int J = 4 * wave_u + i;
       const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
       const int srow = min(row, lim - 1);
-      const int sch = isv ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
-      const f16_t* src = (isv ? kv.v : kv.k) + base + (size_t)srow * kHeadDim + sch * 8;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (LDS_AS void*)(img + isv * 16384 + 4 * (J & 15) * 256), 16, 0, 0);
+      const int sch = dma_v ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
+      dma16_opaque(page + srow * kHeadDim + sch * 8, img + 4 * (J & 15) * 256);
     }
   };
   // Lockstep: every wave runs QK, softmax and PV of tile t between two barriers.  A staggered
   // schedule (wave groups w < 4 and w >= 4, which share SIMDs, one phase apart so one wave's
   // QK MFMAs run beside the other's softmax) measured slower: 356 vs 295 us per layer at
   // configs[1] (two barriers and half-tile DMA waits per tile; profiles/r04/v5_*).
-  dma_tile(0, 0);
+  // page ids run one tile ahead of the DMAs: tile t+1's DMA never waits on a table load
+  dma_tile(page_of(0), 0, 0);
+  int pid_next = ntiles > 1 ? page_of(1) : 0;
   for (int t = 0; t < ntiles; ++t) {
-    // tile t landed (its DMA is the only global load in flight), and every wave is past
-    // tile t-1, whose buffer the next DMA overwrites
+    // tile t landed (its DMA and the next page id are the only global loads in flight), and
+    // every wave is past tile t-1, whose buffer the next DMA overwrites
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t + 1 < ntiles) dma_tile(t + 1, (t + 1) & 1);
+    if (t + 1 < ntiles) {
+      dma_tile(pid_next, t + 1, (t + 1) & 1);
+      pid_next = t + 2 < ntiles ? page_of(t + 2) : 0;
+    }
     if (!wave_live || t * 64 > wave_qlast) continue;  // wave-uniform: keys after every query
     const char* ks_ = smem + (t & 1) * 32768;
     const char* vs_ = ks_ + 16384;
