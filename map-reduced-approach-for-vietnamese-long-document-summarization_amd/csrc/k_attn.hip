@@ -25,6 +25,11 @@ namespace ms {
 constexpr float kLog2e = 1.4426950408889634f;
 
 __device__ __forceinline__ int k_swz(int row, int ch) { return row * 256 + ((ch ^ (row & 15)) << 4); }
+// Q image of GB heads, rows interleaved ([row][head][256 B], K's chunk swizzle): the heads of
+// one k-step sit 256 B apart, inside one ds_read_b128's immediate offset -- one address
+// register per k-step instead of one per (head, k-step)
+template <int GB>
+__device__ __forceinline__ int q_swz(int row, int hh, int ch) { return row * (GB * 256) + hh * 256 + ((ch ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_swz(int row, int ch) { return row * 256 + ((ch ^ ((row & 7) << 1)) << 4); }
 
 // A operand of O^T += V^T P^T for d-tile dt, k-step ks: two transposed 4x16 reads.
@@ -164,8 +169,8 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
             ra[p] = pack2h(r0[0], r0[1]);
             rb[p] = pack2h(r1[0], r1[1]);
           }
-          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * t + g)) = uint4{ra[0], ra[1], ra[2], ra[3]};
-          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * (2 + t) + g)) = uint4{rb[0], rb[1], rb[2], rb[3]};
+          *(uint4*)(qimg + q_swz<GB>(qrow_l, hh, 4 * t + g)) = uint4{ra[0], ra[1], ra[2], ra[3]};
+          *(uint4*)(qimg + q_swz<GB>(qrow_l, hh, 4 * (2 + t) + g)) = uint4{rb[0], rb[1], rb[2], rb[3]};
         }
       }
     } else {
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       for (int hh = 0; hh < GB; ++hh)
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          *(uint4*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
+          *(uint4*)(qimg + q_swz<GB>(qrow_l, hh, 4 * s + g)) = *(const uint4*)(qrow + hh * kHeadDim + 32 * s + 8 * g);
     }
   }
   f32x4 o[GB][8];
@@ -233,18 +238,33 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
     const char* ks_ = smem + (t & 1) * 32768;
     const char* vs_ = ks_ + 16384;
 
+    // S^T by k-step s outermost: the 4 x GB accumulators of a step are independent MFMAs,
+    // and step s+1's K / Q fragments are read from LDS under step s's
     f32x4 sc[GB][4];
+    f16x8 kf[2][4], qf[2][GB];
+    auto rd_step = [&](int s, int b) {
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt) {
+      for (int mt = 0; mt < 4; ++mt) kf[b][mt] = *(const f16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
 #pragma unroll
-      for (int hh = 0; hh < GB; ++hh) sc[hh][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int hh = 0; hh < GB; ++hh) qf[b][hh] = *(const f16x8*)(qimg + q_swz<GB>(qrow_l, hh, 4 * s + g));
+    };
+    rd_step(0, 0);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const f16x8 kf = *(const f16x8*)(ks_ + k_swz(mt * 16 + r, 4 * s + g));
+    for (int s = 0; s < 4; ++s) {
+      if (s + 1 < 4) rd_step(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
 #pragma unroll
         for (int hh = 0; hh < GB; ++hh)
-          sc[hh][mt] = mfma16(kf, *(const f16x8*)(qimg + hh * (QR * 256) + k_swz(qrow_l, 4 * s + g)), sc[hh][mt]);
-      }
+          sc[hh][mt] = mfma16(kf[s & 1][mt], qf[s & 1][hh], s == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : sc[hh][mt]);
+    }
+    // pin that order (the scheduler otherwise issues each read just before its MFMA and
+    // waits on it): [reads s=0] then per step [reads s+1][4 GB MFMAs of s]
+    __builtin_amdgcn_sched_group_barrier(0x100, 4 + GB, 0);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      if (s + 1 < 4) __builtin_amdgcn_sched_group_barrier(0x100, 4 + GB, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * GB, 0);
     }
     // keys past this query (causal) or past the sequence: only tiles reaching past the wave's
     // first query or the sequence end can hold any
@@ -297,7 +317,8 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
       pf[hh][1] = pack_p(sc[hh][2], sc[hh][3]);
     }
     // (an unconditional multiply -- alpha = 1 exactly unless the max moved -- measured
-    // slower: 312 vs 297 us per layer, profiles/r04/v6_*)
+    // slower: 312 vs 297 us per layer, profiles/r04/v6_*; the exponent arguments and row sums
+    // as v_pk_fma_f32 / v_pk_add_f32 pairs, 45 fewer VALU per tile: 276.9 vs 271.5 us, v20_*)
     if (__ballot(rescale) != 0) {
 #pragma unroll
       for (int hh = 0; hh < GB; ++hh)
