@@ -145,6 +145,8 @@ struct ms_engine {
   // opt-in (MS_MLP_FUSED=1) -- measured no faster than the two launches, 2.158 vs 2.130 ms per
   // decode step at B = 8 (profiles/r04/v13_*).  mlp_sync_d: [0..1] counters, [16] timeout flag
   bool mlp_fuse = false, mlp_used = false;
+  // decode_tail_kernel: the step's greedy ids, argument advance and next embedding in one launch
+  bool tail_fuse = true;
   unsigned* mlp_sync_d = nullptr;
   unsigned* mlp_err_h = nullptr;
   bool mlp_fused(const QSlot* gu, const QSlot* dn, int B) const {
@@ -780,6 +782,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_MLP_FUSED")) E.mlp_fuse = atoi(v) != 0;
+    if (const char* v = getenv("MS_DECODE_TAIL")) E.tail_fuse = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
     // the consumers stage the 256-tile statistics in LDS: engines of <= 16 slots (per engine,
@@ -1312,13 +1315,38 @@ static void prefill(ms_engine& E, std::vector<Seq*>& batch, int n_layers_run, fl
   HIP_OK(hipMemcpyAsync(E.first_host, E.ids_out_d, S * sizeof(int32_t), hipMemcpyDeviceToHost, E.stream));
 }
 
-// kernels of one decode step (no host synchronisation: capturable into a hipGraph)
-static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& da) {
-  const size_t o_ids = 0, o_pos = B, o_slot = 2 * (size_t)B;
-  PrefillAttnArgs pa{};
+// the first layer's input of a decode step from the ids in the argument blob: x, xb = f16(x * g0)
+// and its statistics (decode_run's first step; every later step gets them from the previous
+// step's tail)
+static void decode_head(ms_engine& E, int B, int32_t* d) {
   E.prof_begin(K_MISC);
-  launch_embed(d + o_ids, B, E.embed, E.H, E.x, E.stream, E.layers[0].attn_norm, E.xb, E.ssq);
+  launch_embed(d, B, E.embed, E.H, E.x, E.stream, E.layers[0].attn_norm, E.xb, E.ssq);
   E.prof_end(K_MISC);
+}
+
+// argmax of the lm_head partials + decode_advance + the next step's decode_head, one launch
+// (MS_DECODE_TAIL=0: the three launches; the same bits either way)
+static void decode_tail(ms_engine& E, int B, int32_t* d, int tiles) {
+  E.prof_begin(K_MISC);
+  if (E.tail_fuse && B <= 256) {
+    launch_decode_tail(E.logits, tiles, d, E.ids_out_d, E.ids_ring_d, B, E.V, E.embed, E.H, E.x,
+                       E.layers[0].attn_norm, E.xb, E.ssq, E.stream);
+    E.prof_end(K_MISC);
+    return;
+  }
+  launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
+  E.prof_end(K_MISC);
+  launch_decode_advance(d, E.ids_out_d, E.ids_ring_d, B, E.V, E.stream);
+  decode_head(E, B, d);
+}
+
+// kernels of one decode step (no host synchronisation: capturable into a hipGraph).  Enters
+// with the step's layer-0 input in x / xb / ssq and leaves the NEXT step's there: the greedy
+// ids, the argument advance and the next embedding gather are one launch (decode_tail_kernel)
+// on the argmax-partials lm_head paths.
+static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& da) {
+  const size_t o_pos = B, o_slot = 2 * (size_t)B;
+  PrefillAttnArgs pa{};
   E.pending_split = 0;
   E.cur_rs = E.norm_rs();
   // every layer leaves xb = f16(x * the next gain) with its deferred scale in cur_rs
@@ -1330,26 +1358,24 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     // no row scale: r > 0 keeps every row's order (the logits themselves are never stored)
     launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream);
     E.prof_end(K_LMHEAD);
-    E.prof_begin(K_MISC);
-    launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
-    E.prof_end(K_MISC);
+    decode_tail(E, B, d, tiles);
+    return;
   } else if (gemv_supported(std::min(B, (int)ms_engine::kMaxGemvRows), E.V, E.H, MS_GEMV_EPI_ARGMAX) &&
              (B <= ms_engine::kMaxGemvRows || E.row_groups(B))) {
     // greedy argmax in the lm_head epilogue: {max, id} per 16-column tile, no logits row
     const int tiles = E.V / 16;
     E.proj(&E.lmq, E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, nullptr, K_LMHEAD,
            sizeof(float2));
-    E.prof_begin(K_MISC);
-    launch_argmax_partials(E.logits, B, tiles, E.ids_out_d, E.stream);
-    E.prof_end(K_MISC);
-  } else {
-    E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD, &rs);
-    E.prof_begin(K_MISC);
-    launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
-    E.prof_end(K_MISC);
+    decode_tail(E, B, d, tiles);
+    return;
   }
-  // the next chained step's arguments, on the device (decode_run)
+  E.gemm_or_gemv(E.xb, E.lm_head, E.logits, B, E.V, E.H, E.V, MS_EPI_STORE_F32, true, K_LMHEAD, &rs);
+  E.prof_begin(K_MISC);
+  launch_argmax(E.logits, B, E.V, E.ids_out_d, E.stream);
+  E.prof_end(K_MISC);
+  // the next chained step's arguments on the device, then its input rows
   launch_decode_advance(d, E.ids_out_d, E.ids_ring_d, B, E.V, E.stream);
+  decode_head(E, B, d);
 }
 
 // k chained greedy decode steps for every sequence of `batch` (B rows of one token each)
@@ -1370,8 +1396,10 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   for (Seq* s : batch) a.push_back(s->slot);        // [2B, 3B) block-table rows
   for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
   a.push_back(0);                                   // [4B]     step of the run (ring row)
+  a.push_back(0);                                   // [4B+1]   decode_tail's arrival ticket
   HIP_OK(hipEventRecord(E.ev_a, E.stream));
   int32_t* d = E.upload_args(a);
+  decode_head(E, B, d);  // the first step's input; each step's tail gathers the next one's
   DecodeAttnArgs da;
   da.seq_len = d + 3 * (size_t)B;
   da.seq_slot = d + 2 * (size_t)B;

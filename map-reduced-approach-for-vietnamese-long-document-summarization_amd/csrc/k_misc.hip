@@ -4,7 +4,7 @@
 // Reference semantics (EXT, inside Ollama for one /api/generate, SURVEY.md §2 table
 // "ggml op replaced"): get_rows, rms_norm+mul, rope (llama3 freq factors), the greedy
 // sampler.  Numerics contract restated in oracle/llama_ref.py.
-#include "kernels.h"
+#include "gemv_common.h"
 
 namespace ms {
 
@@ -78,6 +78,101 @@ void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring,
                            hipStream_t s) {
   if (B <= 0 || B > 256) return;  // callers chain sub-batches of <= 256 rows
   MS_LAUNCH(decode_advance_kernel, dim3(1), dim3(256), 0, s, args, ids_out, ring, B, V);
+}
+
+// One decode step's tail and the next step's head as ONE launch (three before): block b
+// finishes row b's greedy id from the lm_head's {max, id} partials (argmax_partials_kernel's
+// loop and merge: the same id), advances row b's arguments as decode_advance_kernel does, and
+// gathers the next input row -- x[b] = E[id], xg[b] = f16(x * gamma), ssq[b] -- with
+// embed_kernel's arithmetic on threads 0-255 (the same sums in the same order).  The run's
+// step counter args[4B] moves once, by the last block to arrive on the ticket args[4B + 1]
+// (every block has read it before its ticket), which that block zeroes again.
+__global__ __launch_bounds__(1024) void decode_tail_kernel(const float2* __restrict__ part, int tiles,
+                                                           int32_t* __restrict__ args, int32_t* __restrict__ ids_out,
+                                                           int32_t* __restrict__ ring, int B, int V,
+                                                           const f16_t* __restrict__ emb, int H, float* __restrict__ x,
+                                                           const f16_t* __restrict__ gamma, f16_t* __restrict__ xg,
+                                                           float* __restrict__ ssq) {
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  __shared__ int next_id;
+  __shared__ float red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float2* p = part + (size_t)b * tiles;
+  float v = -INFINITY;
+  int idx = 0x7FFFFFFF;
+  for (int t0 = 0; t0 < tiles; t0 += 8 * 1024) {
+    float2 q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int t = t0 + i * 1024 + tid;
+      q[i] = t < tiles ? p[t] : make_float2(-INFINITY, __int_as_float(0x7FFFFFFF));
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) amax_merge_dev(v, idx, q[i].x, __float_as_int(q[i].y));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+  if ((tid & 63) == 0) { sv[tid >> 6] = v; si[tid >> 6] = idx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 16; ++w) amax_merge_dev(v, idx, sv[w], si[w]);
+    const int id = (idx == 0x7FFFFFFF || !__builtin_isfinite(v)) ? -1 : idx;
+    ids_out[b] = id;
+    const int step = args[4 * B];
+    ring[(size_t)step * B + b] = id;
+    const int in = (id >= 0 && id < V) ? id : 0;
+    args[b] = in;
+    args[B + b] += 1;
+    args[3 * B + b] += 1;
+    next_id = in;
+    __threadfence();  // this block's read of the step counter precedes its ticket
+    typedef __attribute__((address_space(1))) unsigned gu32_t;
+    const unsigned arrived =
+        __hip_atomic_fetch_add((gu32_t*)&args[4 * B + 1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (arrived == (unsigned)B - 1) {
+      args[4 * B + 1] = 0;
+      args[4 * B] = step + 1;
+    }
+  }
+  __syncthreads();
+  if (tid < 256) {
+    const f16_t* row = emb + (size_t)next_id * H;
+    float* xo = x + (size_t)b * H;
+    float ss = 0.f;
+    for (int c = tid; c < H / 8; c += 256) {
+      uint4 e = *(const uint4*)(row + c * 8);
+      const uint32_t w[4] = {e.x, e.y, e.z, e.w};
+      float4 a, bb;
+      a.x = h_lo(w[0]); a.y = h_hi(w[0]);
+      a.z = h_lo(w[1]); a.w = h_hi(w[1]);
+      bb.x = h_lo(w[2]); bb.y = h_hi(w[2]);
+      bb.z = h_lo(w[3]); bb.w = h_hi(w[3]);
+      *(float4*)(xo + c * 8) = a;
+      *(float4*)(xo + c * 8 + 4) = bb;
+      const uint4 gv = *(const uint4*)(gamma + c * 8);
+      const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
+      uint4 o;
+      o.x = pack2h(a.x * h_lo(gw[0]), a.y * h_hi(gw[0]));
+      o.y = pack2h(a.z * h_lo(gw[1]), a.w * h_hi(gw[1]));
+      o.z = pack2h(bb.x * h_lo(gw[2]), bb.y * h_hi(gw[2]));
+      o.w = pack2h(bb.z * h_lo(gw[3]), bb.w * h_hi(gw[3]));
+      *(uint4*)(xg + (size_t)b * H + c * 8) = o;
+      ss += (a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w) + (bb.x * bb.x + bb.y * bb.y + bb.z * bb.z + bb.w * bb.w);
+    }
+    ss = wave_sum(ss);
+    if ((tid & 63) == 0) red[tid >> 6] = ss;
+  }
+  __syncthreads();
+  if (tid == 0) ssq[b] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+void launch_decode_tail(const void* partials, int tiles, int32_t* args, int32_t* ids_out, int32_t* ring, int B,
+                        int V, const f16_t* emb, int H, float* x, const f16_t* gamma, f16_t* xg, float* ssq,
+                        hipStream_t s) {
+  if (B <= 0 || tiles <= 0) return;
+  MS_LAUNCH(decode_tail_kernel, dim3(B), dim3(1024), 0, s, (const float2*)partials, tiles, args, ids_out, ring, B, V,
+            emb, H, x, gamma, xg, ssq);
 }
 
 void launch_embed(const int32_t* ids, int T, const f16_t* emb, int H, float* x, hipStream_t s,

@@ -71,6 +71,11 @@ void launch_embed(const int32_t* ids, int T, const f16_t* emb, int H, float* x, 
 // raw ids appended to ring row `step` (B <= 256)
 void launch_decode_advance(int32_t* args, const int32_t* ids_out, int32_t* ring, int B, int V,
                            hipStream_t s);
+// launch_argmax_partials + launch_decode_advance + the next step's launch_embed (with gamma) as
+// one launch, bit-identical; the blob carries a ticket word args[4B + 1] (zero between steps)
+void launch_decode_tail(const void* partials, int tiles, int32_t* args, int32_t* ids_out, int32_t* ring, int B,
+                        int V, const f16_t* emb, int H, float* x, const f16_t* gamma, f16_t* xg, float* ssq,
+                        hipStream_t s);
 // the GEMM input of a normalised projection: y[r] = f16(x[row_idx[r]] * w), ssq[r] = sum of
 // x[row_idx[r]]^2 (one-tile RowScale); row_idx optional (gather)
 void launch_rmsnorm(const float* x, const f16_t* w, f16_t* y, float* ssq, int rows, int H,
