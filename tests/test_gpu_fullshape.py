@@ -438,6 +438,26 @@ def test_fused_decode_mlp_bit_exact(dev, chunks, monkeypatch):
     assert outs[0] == outs[1]
 
 
+@pytest.mark.parametrize("slots", [NCHUNK, 32])
+def test_decode_tail_bit_exact(dev, chunks, monkeypatch, slots):
+    """The one-launch decode step tail (k_misc.hip decode_tail_kernel: the lm_head partials'
+    argmax, the chained-step advance with its last-arrival step ticket, the next step's
+    embedding and first-norm statistics) against the three launches it replaces: identical
+    greedy ids over chained runs, on the GEMV lm_head (8 slots) and the skinny-GEMM one
+    (32 slots, >= 24: the large regime)."""
+    outs = []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("MS_DECODE_TAIL", fused)
+        e = Engine(CFG, device=0, max_batch=slots, max_ctx=P + 64, max_prefill_tokens=NCHUNK * P)
+        try:
+            e.init_synthetic(SEED, STD, JIT)
+            res = e.generate(list(chunks), num_predict=40, ignore_eos=True)
+            outs.append([r.ids for r in res])
+        finally:
+            e.close()
+    assert outs[0] == outs[1]
+
+
 def test_prefill_packing_invariance(dev):
     """A prompt's prefill does not depend on what it is packed with: alone (600 rows: the
     128x128 GEMM tile) and behind a 1500-token prompt (2100 rows: the 256x256 tile) its hidden
