@@ -218,8 +218,9 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
 int ms_gemm_resid_tiles(int32_t M, int32_t N);
 /* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase) */
 int ms_set_gemm_variant(int32_t variant);
-/* tuning/test hook: the Q6_K lm_head argmax GEMV as a grid-stride two-stage loop (1, the
-   default) or one-tile blocks (0); the two give bit-identical partials */
+/* tuning/test hook: the K-quant GEMVs that have a grid-stride two-stage form (the Q6_K lm_head
+   argmax, the Q4_K gate/up SwiGLU) take it (1, the default) or run one-tile blocks (0); the
+   two give bit-identical outputs */
 int ms_set_qgemv_gs(int32_t on);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);

@@ -465,17 +465,123 @@ __global__ __launch_bounds__(768) __attribute__((amdgpu_waves_per_eu(6, 8))) voi
   }
 }
 
-// whether the Q6_K lm_head takes the grid-stride form (MS_QGEMV_GS=0 / ms_set_qgemv_gs(0):
-// one-tile blocks)
-static int g_q6_gs = -1;
-void set_qgemv_gs(bool on) { g_q6_gs = on ? 1 : 0; }
-static bool q6_gs_on() {
-  if (g_q6_gs < 0) {
-    const char* e = getenv("MS_QGEMV_GS");
-    g_q6_gs = (!e || atoi(e) != 0) ? 1 : 0;
-  }
-  return g_q6_gs != 0;
+// ---- the Q4_K gate/up projection (SwiGLU epilogue) in the same grid-stride form: 256 blocks
+// of 12 waves (wave w = super-block w of the 3072-long rows) take X into registers ONCE (the
+// one-tile kernel's 512 blocks each re-read the 8 x 3072 X -- 49 MB of L2 traffic against
+// 28 MB of weights), then walk 32-row tiles (16 gate + 16 up rows) with the next tile's 6
+// weight loads per lane in flight under the current tile's dequant.  Per tile the arithmetic
+// is qgemv_kernel<1, 2, SWIGLU, 1, REGS, RS>'s exactly: bit-identical outputs.
+struct Q4Regs {
+  uint4 hq, q0, q1;
+};
+__device__ __forceinline__ void q4_fetch(Q4Regs& r, const uint8_t* base, int row_bytes, int row, int sb, int g) {
+  const uint8_t* bp = base + (size_t)row * row_bytes + (size_t)sb * kQ4KBytes;
+  r.hq = ldw16(bp);
+  r.q0 = ldw16(bp + 16 + 32 * g);
+  r.q1 = ldw16(bp + 32 + 32 * g);
 }
+__global__ __launch_bounds__(768) void qgemv_q4_swiglu_gs_kernel(const f16_t* __restrict__ X, QMat qm,
+                                                                 f16_t* __restrict__ out, int M, int N, int K,
+                                                                 int ldo, int rinv_off, GemvArgs ga) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NT = 2, ELEMS = NT * 256;  // MT = 1
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int tiles = N / 32, G = gridDim.x;
+  const uint8_t* base = qm.base0;
+  const int row_bytes = qm.row_bytes0, row0 = qm.row0_0;
+  const bool rs_on = ga.rs.ssq != nullptr;
+  if (rs_on) rs_begin<false>(smem, rinv_off, ga.rs, M);
+  // this wave's super-block of X (qgemv_kernel's kXRegs load, SBW = 1, MT = 1)
+  f16x8 xr[8];
+  const f16_t* xrow = X + (size_t)min(fr, M - 1) * K;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) xr[t] = as_f16x8(ldg16(xrow + (wave * 8 + t) * 32 + 8 * g));
+  __builtin_amdgcn_sched_barrier(0);
+  Q4Regs cur[NT], nxt[NT];
+  int t = blockIdx.x;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) q4_fetch(cur[n], base, row_bytes, t * 32 - row0 + n * 16 + fr, wave, g);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * NT));  // X and the statistics landed (issued first)
+  __builtin_amdgcn_s_barrier();
+  const float* rinv = (const float*)(smem + rinv_off);
+  if (rs_on) rs_finish<false>(smem, rinv_off, ga.rs, M, 0.f);
+  lds_sync();
+  float* red = (float*)smem;
+  typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+  const f16x8 ones = __builtin_bit_cast(f16x8, u4v{0x3C003C00u, 0x3C003C00u, 0x3C003C00u, 0x3C003C00u});
+  for (; t < tiles; t += G) {
+    const bool more = t + G < tiles;
+    if (more) {
+#pragma unroll
+      for (int n = 0; n < NT; ++n) q4_fetch(nxt[n], base, row_bytes, (t + G) * 32 - row0 + n * 16 + fr, wave, g);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) __builtin_amdgcn_s_waitcnt(vmcnt_imm(3 * NT));
+    else __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+    f32x4 acc[NT];
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s_ = 0; s_ < 8; ++s_) {
+      const int sh = 8 * (s_ & 3);
+      const f16x8 xf = xr[s_];
+      const f32x4 xs = mfma16(xf, ones, f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        const uint4 h = cur[n].hq;
+        const uint32_t scw = s_ < 4 ? (h.y & 0x3F3F3F3Fu) : ((h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u));
+        const uint32_t mw = s_ < 4 ? (h.z & 0x3F3F3F3Fu) : (((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u));
+        const float d1 = __fmul_rn(h2f_lo(h.x), (float)((scw >> sh) & 0xFFu));
+        const float m1 = __fmul_rn(h2f_lo(h.x >> 16), (float)((mw >> sh) & 0xFFu));
+        const float d1s = d1 * 16777216.0f;
+        const uint4 qq = s_ < 4 ? cur[n].q0 : cur[n].q1;
+        const int si = s_ & 3;
+        const uint32_t qw = si == 0 ? qq.x : si == 1 ? qq.y : si == 2 ? qq.z : qq.w;
+        const uint32_t lo = qw & 0x0F0F0F0Fu, hi = (qw >> 4) & 0x0F0F0F0Fu;
+        const u4v pk = {__builtin_amdgcn_perm(0u, lo, 0x0C010C00u), __builtin_amdgcn_perm(0u, lo, 0x0C030C02u),
+                        __builtin_amdgcn_perm(0u, hi, 0x0C010C00u), __builtin_amdgcn_perm(0u, hi, 0x0C030C02u)};
+        const f32x4 A = mfma16(xf, __builtin_bit_cast(f16x8, pk), f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[n][i] = __fmaf_rn(-m1, xs[i], __fmaf_rn(d1s, A[i], acc[n][i]));
+      }
+    }
+    // cross-wave reduction and the SwiGLU epilogue (gemv_epilogue's order), LDS-only barriers
+#pragma unroll
+    for (int n = 0; n < NT; ++n) *(f32x4*)&red[wave * ELEMS + (n * 64 + lane) * 4] = acc[n];
+    lds_sync();
+    if ((int)threadIdx.x < 256) {
+      const int e = threadIdx.x, l = (e >> 2) & 63, j = e & 3;
+      const int row = 4 * (l >> 4) + j;
+      if (row < M) {
+        const float rv = rs_on ? rinv[row] : 1.0f;
+        float gs = 0.f, us = 0.f;
+        for (int q = 0; q < nw; ++q) gs += red[q * ELEMS + (0 * 64 + l) * 4 + j];
+        for (int q = 0; q < nw; ++q) us += red[q * ELEMS + (1 * 64 + l) * 4 + j];
+        const float gv = gs * rv, uv = us * rv;
+        out[(size_t)row * ldo + t * 16 + (l & 15)] = f2h(gv / (1.0f + __expf(-gv)) * uv);
+      }
+    }
+    lds_sync();  // red is rewritten by the next tile
+#pragma unroll
+    for (int n = 0; n < NT; ++n) cur[n] = nxt[n];
+  }
+}
+
+// which K-quant GEMVs take the grid-stride form: MS_QGEMV_GS bit 0 the Q6_K lm_head argmax,
+// bit 1 the Q4_K gate/up (default: both; ms_set_qgemv_gs(0): one-tile blocks everywhere)
+static int g_q_gs = -1;
+void set_qgemv_gs(bool on) { g_q_gs = on ? 3 : 0; }
+static int q_gs_mask() {
+  if (g_q_gs < 0) {
+    const char* e = getenv("MS_QGEMV_GS");
+    g_q_gs = e ? atoi(e) : 3;
+  }
+  return g_q_gs;
+}
+static bool q6_gs_on() { return (q_gs_mask() & 1) != 0; }
+static bool q4_gs_on() { return (q_gs_mask() & 2) != 0; }
 
 struct QPlan {
   int MT, NT, SBW, waves, tiles;
@@ -582,8 +688,9 @@ void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K,
   if (p.waves == 0) return;  // callers check qgemv_supported()
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
+  // (both grid-stride kernels finish a tile with one thread per element: >= 4 waves)
   if (epi == MS_GEMV_EPI_ARGMAX && q6_gs_on() && q.n == 1 && q.type0 == MS_QT_Q6_K && p.MT == 1 && p.SBW == 1 &&
-      N % 16 == 0) {
+      p.waves >= 4 && N % 16 == 0) {
     ga.rs = RowScale{};  // as qgemv_go: a row's positive scale never moves its argmax
     // LDS: [X image][per-wave partials][rinv][staged statistics]
     const int red_off = (int)((gemv_x_lds_bytes(M, K) + 15) / 16 * 16);
@@ -594,6 +701,19 @@ void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K,
       const int grid = std::min(N / 16, 512);  // two resident blocks per CU
       MS_LAUNCH(qgemv_q6_argmax_gs_kernel, dim3(grid), dim3(64 * p.waves), lds, s, X, q, (float2*)out, M, N, K, ldo,
                 red_off, ro, ga);
+      return;
+    }
+  }
+  if (epi == MS_GEMV_EPI_SWIGLU && q4_gs_on() && q.n == 1 && q.type0 == MS_QT_Q4_K && p.MT == 1 && p.SBW == 1 &&
+      p.NT == 2 && p.waves >= 4 && qx_in_regs(p) && N % 32 == 0) {
+    if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
+    const size_t main_bytes = (size_t)p.waves * 2 * 256 * 4;  // the per-wave partials
+    const int ro = (int)gemv_rinv_offset(main_bytes);
+    const size_t lds = gemv_lds_total(main_bytes, ga.rs, M);
+    if (lds <= kLdsCap) {
+      const int grid = std::min(N / 32, 256);  // one 12-wave block per CU
+      MS_LAUNCH(qgemv_q4_swiglu_gs_kernel, dim3(grid), dim3(64 * p.waves), lds, s, X, q, (f16_t*)out, M, N, K,
+                ldo, ro, ga);
       return;
     }
   }

@@ -873,6 +873,37 @@ def test_q6_lm_head_grid_stride_bit_exact(lib, dev, M, N, rs):
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
 
 
+@pytest.mark.parametrize("M,N,K,rs", [(8, 16384, 3072, True), (1, 512, 3072, False), (16, 4096, 3072, True),
+                                      (5, 1056, 3072, True), (16, 1024, 1024, True)])
+def test_q4_gate_up_grid_stride_bit_exact(lib, dev, M, N, K, rs):
+    """The grid-stride Q4_K gate/up GEMV (k_qgemv.hip qgemv_q4_swiglu_gs_kernel: X taken into
+    registers once per block, the next 32-row tile's weights in flight) writes the same SwiGLU
+    outputs, bit for bit, as the one-tile blocks -- with and without the rows' deferred-norm
+    scale, at the MLP's width, at ragged tile counts (33 tiles over 256 blocks) and with the
+    fewest waves the form takes (K = 1024: 4)."""
+    b, wbf, pk = _packed(lib, dev, Q.GGML_TYPE_Q4_K, N, K, 23 + M)
+    g = torch.Generator(device="cpu").manual_seed(N + 3 * M)
+    X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
+    ssq = (torch.rand(M, generator=g) * K + 1.0).to(dev)
+    outs = []
+    for gs in (1, 0):
+        L.check(lib.ms_set_qgemv_gs(gs))
+        out = torch.full((M, N // 2), float("nan"), device=dev, dtype=torch.float16)
+        if rs:
+            L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), 1, K, 1e-5))
+        try:
+            L.check(lib.ms_op_qgemv(X.data_ptr(), Q.GGML_TYPE_Q4_K, pk.data_ptr(), out.data_ptr(), M, N, K, N // 2,
+                                    L.MS_EPI_SWIGLU, _stream()))
+        finally:
+            if rs:
+                L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    L.check(lib.ms_set_qgemv_gs(1))
+    assert not torch.isnan(outs[0].float()).any()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))
+
+
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("N,K,S", [(256, 3072, 6), (512, 3072, 4), (128, 8192, 4), (256, 8192, 2),
