@@ -570,7 +570,11 @@ __global__ __launch_bounds__(768) void qgemv_q4_swiglu_gs_kernel(const f16_t* __
 }
 
 // which K-quant GEMVs take the grid-stride form: MS_QGEMV_GS bit 0 the Q6_K lm_head argmax,
-// bit 1 the Q4_K gate/up (default: both; ms_set_qgemv_gs(0): one-tile blocks everywhere)
+// bit 1 the Q4_K gate/up (default: both; ms_set_qgemv_gs(0): one-tile blocks everywhere).  The
+// same form for the single-type split-K slab projections (O, down: X slice staged once per
+// block) measured slower -- O 5.10 -> 6.04 us, down 8.89 -> 9.4-10.7 us, decode 1.806 -> 1.871
+// ms per Q4_K_M step (profiles/r04/v25_*): those launches are one latency each, and fewer
+// blocks leave fewer weight bytes in flight.
 static int g_q_gs = -1;
 void set_qgemv_gs(bool on) { g_q_gs = on ? 3 : 0; }
 static int q_gs_mask() {
@@ -582,6 +586,7 @@ static int q_gs_mask() {
 }
 static bool q6_gs_on() { return (q_gs_mask() & 1) != 0; }
 static bool q4_gs_on() { return (q_gs_mask() & 2) != 0; }
+
 
 struct QPlan {
   int MT, NT, SBW, waves, tiles;
