@@ -15,7 +15,8 @@
 //     144 B, but the 128 quant bytes are re-ordered so that lane group g of a wave reads,
 //     as 32 contiguous bytes, one dword per sub-block s holding weights 32s+8g .. +7 (byte i =
 //     q[k_i] | q[k_{i+4}] << 4); Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales
-//     16 | d 2 + pad] so every field is 16-B aligned.
+//     16 | d 2 + pad] so every field is 16-B aligned, the ql bytes regrouped so that a wave
+//     load reads 64 contiguous bytes per row (quant_rows_kernel).
 // The fused GEMV streams the blocks HBM -> VGPR (one super-block of 256 weights per row
 // per wave-step) and feeds v_mfma_f32_16x16x32_f16:
 //   * Q4_K, one MFMA per 32-weight sub-block: the nibbles become the fp16 subnormals q 2^-24
@@ -123,7 +124,17 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
         q[16 + t] = (uint8_t)(nib(k) | (nib(k + 4) << 4));
       }
     } else {
-      if (t < braw) q[t] = b[t];  // Q6_K: same field order, d at 208, tail padded below
+      // Q6_K: same fields (qh at 128, scales at 192, d at 208, tail padded), ql regrouped by the
+      // GEMV's lane group g = 2 hh + p: its low-half 16 bytes (raw hh*64 + 16p ..) at 16g and its
+      // high-half 16 bytes (raw hh*64 + 32 + 16p ..) at 64 + 16g -- one wave load instruction
+      // then reads 64 contiguous bytes of each row (one 64-B line) instead of two half lines
+      // (qh is already in that order: raw 128 + hh*32 + 16p = 128 + 16g)
+      if (t < 128) {
+        const int hh = t >> 6, half = (t >> 5) & 1, p = (t >> 4) & 1, i = t & 15;
+        q[half * 64 + 16 * (2 * hh + p) + i] = b[t];
+      } else if (t < braw) {
+        q[t] = b[t];
+      }
       if (t >= braw && t < kQ6KPacked) q[t] = 0;
     }
   }
@@ -303,8 +314,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
         const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ6KPacked;
-        qa[j][n] = ldw16(bp + hh * 64 + 16 * p);
-        qb[j][n] = ldw16(bp + hh * 64 + 32 + 16 * p);
+        qa[j][n] = ldw16(bp + 16 * g);  // raw ql hh*64 + 16p .. (quant_rows_kernel's regrouping)
+        qb[j][n] = ldw16(bp + 64 + 16 * g);  // raw ql hh*64 + 32 + 16p ..
         qh[j][n] = ldw16(bp + 128 + hh * 32 + 16 * p);
         sc[j][n] = ldw16(bp + 192);
         dw[j][n] = *(const uint32_t*)(bp + 208);
@@ -376,8 +387,8 @@ struct Q6Regs {
 __device__ __forceinline__ void q6_fetch(Q6Regs& r, const uint8_t* base, int row_bytes, int n0, int fr, int sb,
                                          int hh, int p) {
   const uint8_t* bp = base + (size_t)(n0 + fr) * row_bytes + (size_t)sb * kQ6KPacked;
-  r.qa = ldw16(bp + hh * 64 + 16 * p);
-  r.qb = ldw16(bp + hh * 64 + 32 + 16 * p);
+  r.qa = ldw16(bp + 32 * hh + 16 * p);  // = 16 g: quant_rows_kernel's ql regrouping
+  r.qb = ldw16(bp + 64 + 32 * hh + 16 * p);
   r.qh = ldw16(bp + 128 + hh * 32 + 16 * p);
   r.sc = ldw16(bp + 192);
   r.dw = *(const uint32_t*)(bp + 208);
