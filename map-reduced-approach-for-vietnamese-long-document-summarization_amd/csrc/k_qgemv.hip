@@ -12,9 +12,9 @@
 //     and the embedding gather (compute-bound; fp16 is what MFMA consumes), and
 //   * the quantised rows for decode, which is HBM-bound: 4.5 / 6.56 bits per weight
 //     instead of 16.  Q4_K blocks keep their 16-B ggml header (d, dmin, 12 scale bytes) and
-//     144 B, but the 128 quant bytes are re-ordered so that lane group g of a wave reads,
-//     as 32 contiguous bytes, one dword per sub-block s holding weights 32s+8g .. +7 (byte i =
-//     q[k_i] | q[k_{i+4}] << 4); Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales
+//     144 B, but the 128 quant bytes are re-ordered so that lane group g of a wave reads one
+//     dword per sub-block s holding weights 32s+8g .. +7 (byte i = q[k_i] | q[k_{i+4}] << 4),
+//     sub-blocks 0-3 of the 4 groups in 64 contiguous bytes, then 4-7; Q6_K blocks are repacked to 224 B [ql 128 | qh 64 | scales
 //     16 | d 2 + pad] so every field is 16-B aligned, the ql bytes regrouped so that a wave
 //     load reads 64 contiguous bytes per row (quant_rows_kernel).
 // The fused GEMV streams the blocks HBM -> VGPR (one super-block of 256 weights per row
@@ -112,7 +112,9 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
     const int bp = (type == MS_QT_Q4_K) ? kQ4KBytes : kQ6KPacked;
     uint8_t* q = dst_q + ((drow - q_row_base) * nsb + sb) * bp;
     if (type == MS_QT_Q4_K) {
-      // header as is; quant byte 16 + 4(8g + s) + i = q[k] | q[k + 4] << 4, k = 32s + 8g + i
+      // header as is; quant byte 16 + 64(s >> 2) + 16g + 4(s & 3) + i = q[k] | q[k + 4] << 4,
+      // k = 32s + 8g + i: lane group g's sub-blocks 0-3 at 16 + 16g, 4-7 at 80 + 16g, so one wave
+      // load instruction reads 64 contiguous bytes of each row
       if (t < 16) q[t] = b[t];
       if (t < 128) {
         const int g = t >> 5, s_ = (t >> 2) & 7, i = t & 3;
@@ -121,7 +123,7 @@ __global__ __launch_bounds__(256) void quant_rows_kernel(int type, const uint8_t
           return ((k & 63) >> 5) ? (qb >> 4) : (qb & 0xF);
         };
         const int k = 32 * s_ + 8 * g + i;
-        q[16 + t] = (uint8_t)(nib(k) | (nib(k + 4) << 4));
+        q[16 + 64 * (s_ >> 2) + 16 * g + 4 * (s_ & 3) + i] = (uint8_t)(nib(k) | (nib(k + 4) << 4));
       }
     } else {
       // Q6_K: same fields (qh at 128, scales at 192, d at 208, tail padded), ql regrouped by the
@@ -257,8 +259,8 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
       for (int n = 0; n < NT; ++n) {
         const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ4KBytes;
         hq[j][n] = ldw16(bp);
-        q0[j][n] = ldw16(bp + 16 + 32 * g);
-        q1[j][n] = ldw16(bp + 32 + 32 * g);
+        q0[j][n] = ldw16(bp + 16 + 16 * g);  // sub-blocks 0-3 (quant_rows_kernel's layout)
+        q1[j][n] = ldw16(bp + 80 + 16 * g);  // sub-blocks 4-7
       }
     if constexpr (XL) {  // the X image has landed once at most the weight loads are pending
       __builtin_amdgcn_sched_barrier(0);
@@ -488,8 +490,8 @@ struct Q4Regs {
 __device__ __forceinline__ void q4_fetch(Q4Regs& r, const uint8_t* base, int row_bytes, int row, int sb, int g) {
   const uint8_t* bp = base + (size_t)row * row_bytes + (size_t)sb * kQ4KBytes;
   r.hq = ldw16(bp);
-  r.q0 = ldw16(bp + 16 + 32 * g);
-  r.q1 = ldw16(bp + 32 + 32 * g);
+  r.q0 = ldw16(bp + 16 + 16 * g);
+  r.q1 = ldw16(bp + 80 + 16 * g);
 }
 __global__ __launch_bounds__(768) void qgemv_q4_swiglu_gs_kernel(const f16_t* __restrict__ X, QMat qm,
                                                                  f16_t* __restrict__ out, int M, int N, int K,
