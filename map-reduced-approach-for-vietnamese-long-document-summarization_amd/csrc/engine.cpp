@@ -136,9 +136,7 @@ struct ms_engine {
   // and per-tile sums of x^2 (ssq [256][B]) -- so the decode layer has no residual_rmsnorm
   // launch: the deferred RMSNorm (kernels.h RowScale) scales the rows of the QKV / gate-up /
   // lm_head outputs instead.  Chosen per engine (MS_RESID_FUSED=0: split-K slabs + norm
-  // launches, the K-quant and large-regime form: the K-quant GEMV with this epilogue on 12-row
-  // tiles measured no faster than split-K 4 + residual_rmsnorm, 1.962 vs 1.955 ms per Q4_K_M
-  // decode step, profiles/r03/v7_q4_resid_fused_rejected.txt).
+  // launches, the large-regime form; K-quant engines take it too, below: qresid).
   bool resid_fuse = true, has_quant = false;
   // the layer's decode MLP as one launch (k_mlp.hip: gate/up, a chip-wide hand-off of h, down
   // + residual; bit-identical to the two launches), engines of <= 8 slots on fp16 MLP weights:
@@ -150,12 +148,17 @@ struct ms_engine {
   unsigned* mlp_sync_d = nullptr;
   unsigned* mlp_err_h = nullptr;
   bool mlp_fused(const QSlot* gu, const QSlot* dn, int B) const {
-    return mlp_fuse && resid_fused(gu) && resid_fused(dn) && cfg.max_batch <= 8 &&
+    return mlp_fuse && !(gu && gu->ready()) && resid_fused(gu) && resid_fused(dn) && cfg.max_batch <= 8 &&
            mlp_decode_supported(B, H, F, H / resid_rt);
   }
   int resid_rt = 12;
+  // K-quant O / down with the same epilogue (the Q-GEMV on resid_rt-row tiles; MS_QRESID=0:
+  // split-K 4 + residual_rmsnorm): 1.785 vs 1.794 ms per Q4_K_M decode step -- O 5.8 vs 4.8 +
+  // 4.7 us, down 12.8 vs 8.8 + 4.7 us, the gate/up folding 256 statistics tiles +0.9 us
+  // (profiles/r04/v31_*; round 3 measured it even before the Q-GEMV rewrites)
+  bool qresid = true;
   bool resid_fused(const QSlot* q) const {
-    return resid_fuse && !large_engine && !(q && q->ready());
+    return resid_fuse && !large_engine && (!(q && q->ready()) || qresid);
   }
   // the large-batch arithmetic (skinny GEMM on the fp16 weights) for engines of >= dgemm_min
   // slots -- except engines with K-quant weights: they keep the exact Q4_K / Q6_K GEMV at every
@@ -423,7 +426,10 @@ struct ms_engine {
       ga.gamma = g_next;
       ga.xg_out = xb;
       prof_begin(K_GEMV);
-      launch_gemv_ex(X, W, x, B, H, K, H, MS_GEMV_EPI_RESID_SSQ, &ga, 0, stream);
+      if (q && q->ready())
+        launch_qgemv(X, q->m, x, B, H, K, H, MS_GEMV_EPI_RESID_SSQ, &ga, stream);
+      else
+        launch_gemv_ex(X, W, x, B, H, K, H, MS_GEMV_EPI_RESID_SSQ, &ga, 0, stream);
       prof_end(K_GEMV);
       pending_split = 0;
       cur_rs = make_row_scale(ssq, H / resid_rt, H, cfg.norm_eps);
@@ -783,6 +789,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_MLP_FUSED")) E.mlp_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_DECODE_TAIL")) E.tail_fuse = atoi(v) != 0;
+    if (const char* v = getenv("MS_QRESID")) E.qresid = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
     // the consumers stage the 256-tile statistics in LDS: engines of <= 16 slots (per engine,

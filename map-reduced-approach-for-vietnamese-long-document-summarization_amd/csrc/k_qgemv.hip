@@ -216,7 +216,12 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
   }
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16 * NT;
+  // RESID_SSQ: ga.rt weight rows per tile (lanes fr >= rt load the last row again, never stored)
+  constexpr bool RESID = EPI == MS_GEMV_EPI_RESID_SSQ;
+  const int rt = RESID && ga.rt > 0 ? ga.rt : 16;
+  const int n0 = RESID ? blockIdx.x * rt : blockIdx.x * 16 * NT;
+  const int frw = RESID ? min(fr, rt - 1) : fr;  // this lane's weight row in the tile
+  const ResidPre pre = resid_prefetch<EPI>(M, N, ldo, out, n0, ga);
   // the region holding this tile (regions are 16-row aligned; block-uniform)
   int type = qm.type0, row_bytes = qm.row_bytes0, rbase = n0 - qm.row0_0;
   const uint8_t* base = qm.base0;
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ4KBytes;
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + frw) * row_bytes + (size_t)(sbk + sb0 + j) * kQ4KBytes;
         hq[j][n] = ldw16(bp);
         q0[j][n] = ldw16(bp + 16 + 16 * g);  // sub-blocks 0-3 (quant_rows_kernel's layout)
         q1[j][n] = ldw16(bp + 80 + 16 * g);  // sub-blocks 4-7
@@ -315,7 +320,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
     for (int j = 0; j < SBW; ++j)
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
-        const uint8_t* bp = base + (size_t)(rbase + n * 16 + fr) * row_bytes + (size_t)(sbk + sb0 + j) * kQ6KPacked;
+        const uint8_t* bp = base + (size_t)(rbase + n * 16 + frw) * row_bytes + (size_t)(sbk + sb0 + j) * kQ6KPacked;
         qa[j][n] = ldw16(bp + 16 * g);  // raw ql hh*64 + 16p .. (quant_rows_kernel's regrouping)
         qb[j][n] = ldw16(bp + 64 + 16 * g);  // raw ql hh*64 + 32 + 16p ..
         qh[j][n] = ldw16(bp + 128 + hh * 32 + 16 * p);
@@ -370,7 +375,7 @@ __global__ __launch_bounds__(1024) void qgemv_kernel(const f16_t* __restrict__ X
         }
       }
   }
-  gemv_finish<MT, NT, EPI, RS>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, ResidPre{0.f, 0.f}, rsd);
+  gemv_finish<MT, NT, EPI, RS>(acc, smem, rinv_off, M, N, ldo, out, n0, ga, pre, rsd);
 }
 
 // ---- the Q6_K lm_head (greedy argmax partials) as a grid-stride two-stage loop.  One-tile
@@ -605,11 +610,12 @@ struct QPlan {
   int MT, NT, SBW, waves, tiles;
 };
 
-static QPlan qplan(int M, int N, int K, int epi) {  // K: per-split length
+static QPlan qplan(int M, int N, int K, int epi, int rt = 0) {  // K: per-split length
   QPlan p{};
   p.MT = (M + 15) / 16;
   p.NT = (epi == MS_GEMV_EPI_SWIGLU) ? 2 : 1;
-  p.tiles = (N + 16 * p.NT - 1) / (16 * p.NT);
+  const int rows = epi == MS_GEMV_EPI_RESID_SSQ && rt > 0 ? rt : 16 * p.NT;
+  p.tiles = (N + rows - 1) / rows;
   const int nsb = K / 256;
   p.SBW = nsb > 16 ? 2 : 1;
   p.waves = (nsb % p.SBW == 0) ? nsb / p.SBW : 0;
@@ -641,8 +647,10 @@ static size_t qlds(const QPlan& p, int M, int K, const RowScale& rs = RowScale{}
 
 bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles) {
   if (M < 1 || M > 64 || K % 256 || N % 16) return false;
-  if (epi == MS_GEMV_EPI_ROPE_KV && M > 16) return false;
+  if ((epi == MS_GEMV_EPI_ROPE_KV || epi == MS_GEMV_EPI_RESID_SSQ) && M > 16) return false;
   const QPlan p = qplan(M, N, K, epi);
+  // the residual epilogue's prefetch covers one element per thread of a >= 256-thread block
+  if (epi == MS_GEMV_EPI_RESID_SSQ && p.waves < 4) return false;
   RowScale rs{};
   if (rs_tiles > 0 && epi != MS_GEMV_EPI_ARGMAX && epi != MS_GEMV_EPI_ADD_F32) {  // qgemv_go drops it there
     if (!gemv_rs_supported(M, rs_tiles)) return false;
@@ -660,7 +668,7 @@ static void qgemv_go(const f16_t* X, const QMat& q, void* out, int M, int N, int
   const size_t lds = qlds(p, M, K, ga.rs);
   const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
-  if constexpr (EPI == MS_GEMV_EPI_ROPE_KV && MT != 1) {
+  if constexpr ((EPI == MS_GEMV_EPI_ROPE_KV || EPI == MS_GEMV_EPI_RESID_SSQ) && MT != 1) {
     return;
   } else {
     const bool xl = qx_in_lds(M, K);
@@ -695,6 +703,7 @@ static void qgemv_go_mt(const f16_t* X, const QMat& q, void* out, int M, int N, 
     case MS_GEMV_EPI_SWIGLU: qgemv_go<MT, 2, MS_GEMV_EPI_SWIGLU>(X, q, out, M, N, K, ldo, p, ga, s); break;
     case MS_GEMV_EPI_ROPE_KV: qgemv_go<MT, 1, MS_GEMV_EPI_ROPE_KV>(X, q, out, M, N, K, ldo, p, ga, s); break;
     case MS_GEMV_EPI_ARGMAX: qgemv_go<MT, 1, MS_GEMV_EPI_ARGMAX>(X, q, out, M, N, K, ldo, p, ga, s); break;
+    case MS_GEMV_EPI_RESID_SSQ: qgemv_go<MT, 1, MS_GEMV_EPI_RESID_SSQ>(X, q, out, M, N, K, ldo, p, ga, s); break;
     default: qgemv_go<MT, 1, MS_GEMV_EPI_STORE_F32>(X, q, out, M, N, K, ldo, p, ga, s); break;
   }
 }
@@ -702,7 +711,7 @@ static void qgemv_go_mt(const f16_t* X, const QMat& q, void* out, int M, int N, 
 void launch_qgemv(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int ldo, int epi,
                   const GemvArgs* ga_in, hipStream_t s) {
   if (M <= 0) return;
-  const QPlan p = qplan(M, N, K, epi);
+  const QPlan p = qplan(M, N, K, epi, ga_in ? ga_in->rt : 0);
   if (p.waves == 0) return;  // callers check qgemv_supported()
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
