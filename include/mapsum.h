@@ -85,9 +85,11 @@ typedef struct ms_config {
   /* engine */
   int32_t device;               /* HIP device ordinal                         */
   int32_t max_batch;            /* sequences in flight (<= 1024).  Also fixes the
-                                   engine's decode arithmetic (fp16 weights):
+                                   engine's decode arithmetic (fp16 weights:
                                    1-16 residual-fused GEMV, 17-23 split GEMV +
-                                   residual_rmsnorm, >= 24 skinny GEMM; results
+                                   residual_rmsnorm, >= 24 skinny GEMM; K-quant:
+                                   1-16 residual-fused Q-GEMV, >= 17 split
+                                   Q-GEMV + residual_rmsnorm); results
                                    are batch-invariant inside one engine, not
                                    across these boundaries */
   int32_t max_ctx;              /* prompt + generated tokens per sequence     */

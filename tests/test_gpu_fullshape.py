@@ -330,14 +330,16 @@ _Q4_GEN = {}
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("slots", [2, 32, 128])
+@pytest.mark.parametrize("slots", [2, 16, 32, 128])
 def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
     """configs[4] at the full widths (2 layers): Q4_K_M blocks through ms_load_weight_q;
     prefill logits and 64 teacher-forced greedy tokens against the oracle run on the
     dequantised weights.  Every engine size decodes with the dequant-fused K-quant GEMVs
-    (exact Q4_K arithmetic): 2 slots in one row group, 32 and 128 slots (the large-batch regime
-    of fp16 engines) in row groups of <= 64 -- with 96 chunks in flight at 128 slots the batch
-    really spans two groups -- so the chunk's tokens are the same at every engine size."""
+    (exact Q4_K arithmetic): 2 and 16 slots in one row group with the residual epilogue on O /
+    down (engines of <= 16 slots, as fp16), 32 and 128 slots (the large-batch regime of fp16
+    engines) in row groups of <= 64 with split-K O / down -- with 96 chunks in flight at 128
+    slots the batch really spans two groups.  Within a regime the chunk's tokens do not depend
+    on the engine size."""
     from mapsum.weights import load_quantized
     qw, w, o = q4km
     prompt = _chunks()[2][:768]
@@ -357,10 +359,11 @@ def test_fullshape_q4_k_m_engine_vs_oracle(q4km, slots):
         else:
             gen = np.asarray(e.generate([prompt], num_predict=64, ignore_eos=True)[0].ids)
         _Q4_GEN[slots] = gen
-        if 2 in _Q4_GEN and slots == 32:
-            # engine-size invariance: the K-quant GEMV arithmetic is per row, and 2- and 32-slot
-            # engines share the decode-attention plan (2 pages per wave); a 128-slot engine splits
-            # attention at 8 pages per wave (attn_decode_ppw), a different fp32 sum order, so
+        if 2 in _Q4_GEN and slots == 16:
+            # engine-size invariance: the K-quant GEMV arithmetic is per row, and 2- and 16-slot
+            # engines share the residual-epilogue regime and the decode-attention plan (2 pages
+            # per wave); 32 slots sum O / down over split-K slabs, and a 128-slot engine splits
+            # attention at 8 pages per wave (attn_decode_ppw) -- different fp32 sum orders, so
             # there only the oracle check below applies
             assert np.array_equal(gen, _Q4_GEN[2]), (slots, np.nonzero(gen != _Q4_GEN[2])[0][:5])
         tl = _teacher_forced(o, cache, ref_lg[-1], gen)
