@@ -157,8 +157,15 @@ struct ms_engine {
   // 4.7 us, down 12.8 vs 8.8 + 4.7 us, the gate/up folding 256 statistics tiles +0.9 us
   // (profiles/r04/v31_*; round 3 measured it even before the Q-GEMV rewrites)
   bool qresid = true;
+  // the K-quant GEMVs this regime launches support its shapes (ms_create: RESID_SSQ on O / down
+  // and the gate/up SwiGLU folding 256 statistics tiles); the launchers return silently on an
+  // unsupported shape, so an engine whose quantised shapes fall outside the Q plan takes split-K
+  // + residual_rmsnorm instead of skipping the residual update
+  bool qresid_ok = true;
   bool resid_fused(const QSlot* q) const {
-    return resid_fuse && !large_engine && (!(q && q->ready()) || qresid);
+    if (!resid_fuse || large_engine) return false;
+    if (has_quant && !qresid_ok) return false;
+    return !(q && q->ready()) || qresid;
   }
   // the large-batch arithmetic (skinny GEMM on the fp16 weights) for engines of >= dgemm_min
   // slots -- except engines with K-quant weights: they keep the exact Q4_K / Q6_K GEMV at every
@@ -345,8 +352,12 @@ struct ms_engine {
     // epilogue (resid_fused is off in large engines), one residual_rmsnorm over all rows
     if (row_groups(B) && !(B <= kMaxSlabRows && attn_slabs && !resid_fused(nullptr))) return false;
     const int Bg = std::min(B, (int)kMaxGemvRows);
+    // the gate/up GEMV folds the statistics its producer wrote: 256 tiles behind the residual
+    // epilogue, one behind residual_rmsnorm
+    const int gu_tiles = resid_fused(nullptr) ? H / resid_rt : 1;
     return residual_rmsnorm_supported(kMaxSplit, H) &&
-           (attn_slabs ? gemv_split_supported(Bg, QKVN, H, 1) : gemv_supported(Bg, QKVN, H, MS_GEMV_EPI_ROPE_KV)) && gemv_supported(Bg, 2 * F, H, MS_GEMV_EPI_SWIGLU) &&
+           (attn_slabs ? gemv_split_supported(Bg, QKVN, H, 1) : gemv_supported(Bg, QKVN, H, MS_GEMV_EPI_ROPE_KV)) &&
+           gemv_supported(Bg, 2 * F, H, MS_GEMV_EPI_SWIGLU, gu_tiles) &&
            gemv_split_supported(Bg, H, Hq * D, 1) && gemv_split_supported(Bg, H, F, 1) &&
            (!resid_fuse || (gemv_supported(Bg, H, Hq * D, MS_GEMV_EPI_RESID_SSQ) &&
                             gemv_supported(Bg, H, F, MS_GEMV_EPI_RESID_SSQ))) &&
@@ -549,15 +560,24 @@ struct ms_engine {
   // prefill residual update x += X . W^T whose GEMM epilogue also writes xb = f16(x * g_next)
   // and per-column-tile sums of x^2 (k_gemm.hip GemmResid): no norm launch between the
   // residual add and the next normalised projection
+  // The path is picked BEFORE any launch: the epilogue writes [H / 128][T] statistics into ssq
+  // (sized R * kGemmRsTiles), so hidden sizes above 24 * 128 take the plain residual add and
+  // one rmsnorm launch instead (ms_create accepts any hidden % 256 == 0).
+  bool prefill_resid_ok(int T) const {
+    const int tiles = gemm_resid_tiles(T, H);
+    return tiles <= kGemmRsTiles && gemm_rs_tiles_ok(T, QKVN, tiles) && gemm_rs_tiles_ok(T, 2 * F, tiles);
+  }
   void prefill_resid(const f16_t* X, const f16_t* W, int T, int K, const f16_t* g_next) {
+    if (!prefill_resid_ok(T)) {
+      gemm_or_gemv(X, W, x, T, H, K, H, MS_EPI_ADD_F32, false, K_GEMM);
+      norm_input(g_next, T);
+      return;
+    }
     GemmResid gr{g_next, xb, ssq};
     prof_begin(K_GEMM);
     launch_gemm(X, W, x, T, H, K, H, MS_EPI_ADD_F32, stream, nullptr, &gr);
     prof_end(K_GEMM);
-    const int tiles = gemm_resid_tiles(T, H);
-    REQUIRE(gemm_rs_tiles_ok(T, QKVN, tiles) && gemm_rs_tiles_ok(T, 2 * F, tiles), MS_EINVAL,
-            "prefill residual statistics: consumer GEMM cannot fold them");
-    cur_rs = make_row_scale(ssq, tiles, H, cfg.norm_eps);
+    cur_rs = make_row_scale(ssq, gemm_resid_tiles(T, H), H, cfg.norm_eps);
   }
 
   // xb = f16(x * w), ssq = the rows' sums of squares (rmsnorm_kernel), cur_rs = their scale
@@ -795,6 +815,12 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     // the consumers stage the 256-tile statistics in LDS: engines of <= 16 slots (per engine,
     // so every step of it runs the same arithmetic)
     if (!gemv_rs_supported(cfg->max_batch, E.H / E.resid_rt)) E.resid_fuse = false;
+    {
+      const int Bg = std::min(cfg->max_batch, (int)ms_engine::kMaxGemvRows);
+      E.qresid_ok = qgemv_supported(Bg, E.H, E.Hq * E.D, MS_GEMV_EPI_RESID_SSQ) &&
+                    qgemv_supported(Bg, E.H, E.F, MS_GEMV_EPI_RESID_SSQ) &&
+                    qgemv_supported(Bg, 2 * E.F, E.H, MS_GEMV_EPI_SWIGLU, E.H / E.resid_rt);
+    }
     if (const char* v = getenv("MS_GRAPH_STEPS")) E.graph_steps = std::max(1, std::min(atoi(v), 16));
     for (ms_engine::Ctx* c : {&E.cp, &E.cd}) {
       c->args_cap = 8 * T + 64 * (size_t)cfg->max_batch + (size_t)cfg->max_batch * E.max_pages + 1024;
@@ -1448,9 +1474,17 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
   if (E.mlp_used && *E.mlp_err_h) {  // a workgroup of the fused MLP was not resident: never silent
+    // fall back to the two launches for good: clear the device flag and the counters, and drop
+    // every captured graph that still holds mlp_decode_kernel; the run's ids are discarded (the
+    // sequences did not advance), so the next ms_step recomputes them unfused
     E.mlp_fuse = false;
+    E.mlp_used = false;
+    HIP_OK(hipMemsetAsync(E.mlp_sync_d, 0, 64 * sizeof(unsigned), E.stream));
+    HIP_OK(hipStreamSynchronize(E.stream));
+    *E.mlp_err_h = 0;
+    E.drop_graphs();
     REQUIRE(false, MS_EIO, "fused decode MLP: hand-off timed out (not every workgroup resident); "
-                           "fusion disabled for this engine, the step's ids are invalid");
+                           "fusion disabled for this engine, the run's ids were discarded");
   }
   std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));
 }
@@ -1705,7 +1739,7 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
     REQUIRE(!g_op_rs.ssq || gemm_rs_tiles_ok(M, N, g_op_rs.tiles), MS_EINVAL,
-            "gemm row scale: at most 24 tiles of statistics (12 for the 256x256 kernel)");
+            "gemm row scale: at most 24 tiles of statistics (kGemmRsTiles, both GEMM tiles)");
     launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
   });
 }

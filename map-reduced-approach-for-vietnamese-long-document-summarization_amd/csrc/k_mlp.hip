@@ -49,6 +49,7 @@ struct MlpArgs {
   float* x;            // [M][H] fp32 residual
   unsigned* sync;      // [2]: arrivals, departures (zero between launches)
   unsigned* err;       // timeout flag (set, never cleared by the kernel)
+  unsigned spin;       // polls before the hand-off gives up (kSpinLimit; MS_MLP_SPIN for tests)
   GemvArgs gu;         // .rs: the gate/up rows' deferred-norm statistics
   GemvArgs dn;         // .rt = 12, .ssq_out / .gamma / .xg_out: the residual epilogue
   int M, H, F, rinv_off;
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(1024) void mlp_decode_kernel(MlpArgs a) {
   issue_down();
   if (wave == kMlpPollWave) {
     bool ok = false;
-    for (unsigned it = 0; it < kSpinLimit; ++it) {
+    for (unsigned it = 0; it < a.spin; ++it) {
       if (__hip_atomic_load((gu32_t*)&a.sync[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kMlpBlocks) {
         ok = true;
         break;
@@ -246,6 +247,9 @@ void launch_mlp_decode(const f16_t* xb, const f16_t* wgu, const f16_t* wdown, f1
   a.x = x;
   a.sync = sync;
   a.err = err;
+  // MS_MLP_SPIN: the poll bound (0 forces the timeout path: test_fused_decode_mlp_timeout_recovers)
+  const char* sv = getenv("MS_MLP_SPIN");  // read per launch (host side; graphs capture it once)
+  a.spin = sv ? (unsigned)strtoul(sv, nullptr, 10) : kSpinLimit;
   a.gu.rs = rs;
   a.dn.rt = kMlpRt;
   a.dn.ssq_out = ssq_out;

@@ -154,23 +154,63 @@ def set_backend_factory(fn):
     _FACTORY = fn
 
 
-def _default_factory(model_name: str) -> MapBackend:
-    """Real-weight path: MAPSUM_MODEL_DIR (HF Llama-3.2 safetensors + tokenizer.json)."""
-    from .config import LLAMA32_3B
-    from .engine import Engine
-    from .tokenizer import Tokenizer
-    from .weights import load_hf_dir
-    d = os.environ.get("MAPSUM_MODEL_DIR")
-    if not d:
-        raise RuntimeError(f"no backend registered for model {model_name!r} and MAPSUM_MODEL_DIR unset")
+def _engine_kwargs() -> dict:
     # the decode regime is fixed per engine (DESIGN.md §5), so any max_batch keeps a batched
     # call equal to the same call alone; 64 in flight runs the large-batch regime
-    eng = Engine(LLAMA32_3B, device=int(os.environ.get("LOCAL_RANK", 0)),
-                 max_batch=int(os.environ.get("MAPSUM_MAX_BATCH", 64)),
-                 max_ctx=int(os.environ.get("MAPSUM_MAX_CTX", 16384)),
-                 max_prefill_tokens=int(os.environ.get("MAPSUM_MAX_PREFILL", 32768)))
-    load_hf_dir(eng, d)
-    return MapBackend(eng, Tokenizer(os.path.join(d, "tokenizer.json")))
+    return dict(device=int(os.environ.get("LOCAL_RANK", 0)),
+                max_batch=int(os.environ.get("MAPSUM_MAX_BATCH", 64)),
+                max_ctx=int(os.environ.get("MAPSUM_MAX_CTX", 16384)),
+                max_prefill_tokens=int(os.environ.get("MAPSUM_MAX_PREFILL", 32768)))
+
+
+def gguf_backend(path: str, engine_cls=None, params: dict | None = None) -> MapBackend:
+    """A backend on a GGUF file: the model config and the tokenizer both come from the file's
+    own metadata (an Ollama blob has no tokenizer.json), the weights through gguf.load_gguf
+    (F16 / BF16 / F32 as fp16; Q4_K / Q6_K as the dequant-fused K-quant path).  ``params`` is
+    the Ollama manifest's params layer: its single-token ``stop`` strings join the stop set."""
+    from .gguf import load_gguf, read_gguf
+    from .ollama_store import config_from_gguf
+    from .tokenizer import tokenizer_from_gguf
+    if engine_cls is None:
+        from .engine import Engine as engine_cls
+    meta, ts = read_gguf(path)
+    cfg = config_from_gguf(meta).with_(tie_embeddings="output.weight" not in ts)
+    tok = tokenizer_from_gguf(meta)
+    stops = list(cfg.eos_ids)
+    for s in (params or {}).get("stop", []):
+        ids = tok.encode(s, add_bos=False)
+        if len(ids) == 1 and ids[0] not in stops:
+            stops.append(ids[0])
+    del ts
+    eng = engine_cls(cfg, eos_ids=tuple(stops[:8]), **_engine_kwargs())
+    load_gguf(eng, path)
+    return MapBackend(eng, tok)
+
+
+def _default_factory(model_name: str) -> MapBackend:
+    """Real-weight path, in order: MAPSUM_MODEL_DIR (HF Llama-3.2 safetensors + tokenizer.json),
+    MAPSUM_GGUF (a GGUF file), else the Ollama store ($OLLAMA_MODELS or ~/.ollama/models): the
+    tag the reference passes (``llama3.2:3b``, run_full_evaluation_pipeline.py:961) -> manifest
+    -> GGUF blob, exactly the file `ollama serve` would run."""
+    d = os.environ.get("MAPSUM_MODEL_DIR")
+    if d:
+        from .config import LLAMA32_3B
+        from .engine import Engine
+        from .tokenizer import Tokenizer
+        from .weights import load_hf_dir
+        eng = Engine(LLAMA32_3B, **_engine_kwargs())
+        load_hf_dir(eng, d)
+        return MapBackend(eng, Tokenizer(os.path.join(d, "tokenizer.json")))
+    g = os.environ.get("MAPSUM_GGUF")
+    if g:
+        return gguf_backend(g)
+    from . import ollama_store
+    try:
+        m = ollama_store.resolve(model_name)
+    except (FileNotFoundError, ValueError) as e:
+        raise RuntimeError(f"no backend for model {model_name!r}: MAPSUM_MODEL_DIR / MAPSUM_GGUF unset and "
+                           f"the Ollama store has no such model ({e})") from e
+    return gguf_backend(m.gguf, params=m.params)
 
 
 def get_backend(model_name: str) -> MapBackend:

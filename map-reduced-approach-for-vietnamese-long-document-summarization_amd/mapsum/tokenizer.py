@@ -45,3 +45,67 @@ class Tokenizer:
 
     def decode_batch(self, seqs) -> list:
         return self.tk.decode_batch([list(s) for s in seqs], skip_special_tokens=True)
+
+
+# ------------------------------------------------------------------ from GGUF metadata
+# An Ollama install keeps no tokenizer.json: the vocabulary lives in the GGUF blob's metadata
+# (EXT, llama.cpp's converter: tokenizer.ggml.model "gpt2" = byte-level BPE, .pre the
+# pre-tokenizer family, .tokens / .token_type / .merges, .bos/.eos/.eot_token_id), which is
+# what Ollama tokenises with for llama3.2:3b (README.md:32).  The pre-tokenizer regexes are the
+# published ones of each family: "llama-bpe" is Llama-3's tiktoken pattern, as in Meta's
+# tokenizer.json (Split isolated, then ByteLevel without its own regex; BPE with
+# ignore_merges -- a pre-token that is itself a vocabulary entry is not merged further).
+PRE_TOKENIZERS = {
+    "llama-bpe": (r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}{1,3}| ?[^\s\p{L}\p{N}]+[\r\n]*"
+                  r"|\s*[\r\n]+|\s+(?!\S)|\s+", True),
+    "default": (r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+", False),
+}
+TOKEN_CONTROL, TOKEN_USER_DEFINED = 3, 4  # llama.cpp token types matched as special tokens
+
+
+def tokenizer_from_gguf(meta: dict) -> "Tokenizer":
+    """A Tokenizer from a GGUF's tokenizer.ggml.* metadata (byte-level BPE families only)."""
+    from tokenizers import AddedToken, Regex, decoders, models, pre_tokenizers
+    from tokenizers import Tokenizer as _T
+    model = meta.get("tokenizer.ggml.model")
+    if model != "gpt2":
+        raise ValueError(f"GGUF tokenizer model {model!r} is not byte-level BPE ('gpt2')")
+    pre = meta.get("tokenizer.ggml.pre", "default")
+    if pre not in PRE_TOKENIZERS:
+        raise ValueError(f"GGUF pre-tokenizer {pre!r} is not supported ({sorted(PRE_TOKENIZERS)})")
+    pattern, ignore_merges = PRE_TOKENIZERS[pre]
+    tokens = list(meta["tokenizer.ggml.tokens"])
+    types = list(meta.get("tokenizer.ggml.token_type", [1] * len(tokens)))
+    merges = [tuple(m.split(" ", 1)) for m in meta.get("tokenizer.ggml.merges", [])]
+    vocab = {}
+    for i, t in enumerate(tokens):
+        vocab.setdefault(t, i)
+    tk = _T(models.BPE(vocab=vocab, merges=merges, ignore_merges=ignore_merges, fuse_unk=False,
+                       byte_fallback=False))
+    tk.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(pattern), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, trim_offsets=False, use_regex=False)])
+    tk.decoder = decoders.ByteLevel()
+    tk.add_special_tokens([AddedToken(tokens[i], special=True, normalized=False)
+                           for i, ty in enumerate(types) if ty in (TOKEN_CONTROL, TOKEN_USER_DEFINED)])
+    bos = meta.get("tokenizer.ggml.bos_token_id")
+    if not meta.get("tokenizer.ggml.add_bos_token", True):
+        bos = None
+    return Tokenizer.from_object(tk, bos_id=int(bos) if bos is not None else None)
+
+
+def gguf_stop_ids(meta: dict) -> tuple:
+    """End-of-generation ids of a GGUF vocabulary: eos, eot and eom where present (llama.cpp's
+    end-of-generation set; Llama-3.2: <|eot_id|> 128009, <|end_of_text|> 128001, <|eom_id|>)."""
+    out = []
+    for k in ("tokenizer.ggml.eos_token_id", "tokenizer.ggml.eot_token_id", "tokenizer.ggml.eom_token_id"):
+        v = meta.get(k)
+        if v is not None and int(v) not in out:
+            out.append(int(v))
+    tokens = meta.get("tokenizer.ggml.tokens", [])
+    for name in ("<|eot_id|>", "<|eom_id|>", "<|end_of_text|>"):
+        if name in tokens:
+            i = tokens.index(name)
+            if i not in out:
+                out.append(i)
+    return tuple(out[:8])

@@ -102,3 +102,78 @@ def make_weights(cfg, seed: int, std: float = 0.02, jitter: float = 0.0) -> dict
 def f16_rne(x: np.ndarray) -> np.ndarray:
     """float32 -> nearest-even IEEE fp16 (the engine's 16-bit type), returned as float32."""
     return np.asarray(x, dtype=np.float32).astype(np.float16).astype(np.float32)
+
+
+# ----------------------------------------------------------------- synthetic K-quant blocks
+# Restates csrc/k_qgemv.hip synth_qblocks_kernel and engine.cpp ms_init_synthetic_q (the
+# configs[4] bench weights, seed 2): block i of a tensor = the bytes of successive splitmix64
+# states h_{j+1} = smix(h_j), h_0 = smix(i ^ smix(seed ^ tensor << 56 ^ layer << 48)), little
+# endian, 8 per state; then u = 0.5 + (smix(h_last) >> 40) 2^-24 and the fp16 scale fields
+# (Q4_K: d = f16(u scale / 270), dmin = f16(d 7.5); Q6_K: the 16 int8 scales folded into
+# [-64, 63], d = f16(u scale / 680)).
+Q4_K, Q6_K = 12, 14
+_QBYTES = {Q4_K: 144, Q6_K: 210}
+
+
+def synth_qblocks(qtype: int, n_blocks: int, seed: int, tensor: int, layer: int, scale: float = 0.02) -> np.ndarray:
+    """uint8 [n_blocks, block_bytes]: the device generator's blocks of one tensor, bit for bit."""
+    braw = _QBYTES[qtype]
+    seed_h = splitmix64(np.uint64((seed ^ (tensor << 56) ^ (layer << 48)) & 0xFFFFFFFFFFFFFFFF))
+    out = np.empty((n_blocks, braw), np.uint8)
+    step = 1 << 20
+    for b0 in range(0, n_blocks, step):
+        b1 = min(n_blocks, b0 + step)
+        h = splitmix64(np.arange(b0, b1, dtype=np.uint64) ^ seed_h)
+        for k in range(0, braw, 8):
+            h = splitmix64(h)
+            nb = min(8, braw - k)
+            out[b0:b1, k:k + nb] = h.view(np.uint8).reshape(-1, 8)[:, :nb]
+        u = np.float32(0.5) + (splitmix64(h) >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+        blk = out[b0:b1]
+        if qtype == Q4_K:
+            d = ((u * np.float32(scale)) / np.float32(270.0)).astype(np.float16)
+            dm = (d.astype(np.float32) * np.float32(7.5)).astype(np.float16)
+            blk[:, 0:2] = d.view(np.uint8).reshape(-1, 2)
+            blk[:, 2:4] = dm.view(np.uint8).reshape(-1, 2)
+        else:
+            blk[:, 192:208] = ((blk[:, 192:208].astype(np.int32) & 0x7F) - 64).astype(np.int8).view(np.uint8)
+            d = ((u * np.float32(scale)) / np.float32(680.0)).astype(np.float16)
+            blk[:, 208:210] = d.view(np.uint8).reshape(-1, 2)
+    return out
+
+
+def make_q4km_blocks(cfg, seed: int = 2, scale: float = 0.02) -> dict:
+    """{name or (layer, name): (ggml type, blocks)} of ms_init_synthetic_q's Q4_K_M model
+    (tied embedding = lm_head; per-tensor mix oracle/quants.py q4_k_m_type)."""
+    from oracle.quants import q4_k_m_type
+    H, D = cfg.hidden, cfg.head_dim
+    shapes = {"wq": (WQ, cfg.n_heads * D, H), "wk": (WK, cfg.n_kv_heads * D, H), "wv": (WV, cfg.n_kv_heads * D, H),
+              "wo": (WO, H, cfg.n_heads * D), "w_gate": (WGATE, cfg.ffn, H), "w_up": (WUP, cfg.ffn, H),
+              "w_down": (WDOWN, H, cfg.ffn)}
+    qt = q4_k_m_type("embed", 0, cfg.n_layers)
+    qw = {"embed": (qt, synth_qblocks(qt, cfg.vocab * H // 256, seed, EMBED, 0, scale))}
+    for l in range(cfg.n_layers):
+        for name, (kind, r, c) in shapes.items():
+            qt = q4_k_m_type(name, l, cfg.n_layers)
+            qw[(l, name)] = (qt, synth_qblocks(qt, r * c // 256, seed, kind, l, scale))
+    return qw
+
+
+def q4km_weights(cfg, qw: dict, seed: int = 2, jitter: float = 0.0, dequant=None) -> dict:
+    """Logical float32 weights of a Q4_K_M block set: the EXACT fp32 dequantisation (ggml's
+    dequantize_row_*, oracle/ggml_quants.c) -- not rounded to fp16."""
+    if dequant is None:
+        from oracle.quants import c_dequant as dequant
+    H = cfg.hidden
+    qt, eb = qw["embed"]
+    w = {"embed": dequant(eb, qt).reshape(cfg.vocab, H), "final_norm": norm(seed, FINAL_NORM, 0, H, jitter),
+         "layers": []}
+    w["lm_head"] = w["embed"]
+    for l in range(cfg.n_layers):
+        ly = {"attn_norm": norm(seed, ATTN_NORM, l, H, jitter), "ffn_norm": norm(seed, FFN_NORM, l, H, jitter)}
+        for name in ("wq", "wk", "wv", "wo", "w_gate", "w_up", "w_down"):
+            qt, b = qw[(l, name)]
+            r = {"wo": H, "w_down": H}.get(name)
+            ly[name] = dequant(b, qt).reshape(r if r else -1, -1 if r else H)
+        w["layers"].append(ly)
+    return w

@@ -11,7 +11,10 @@ Two models (tests/golden/sharp_model.py explains the second):
   sharp -- seed 77 (norm jitter 0.1) with a RoPE copy head at a late layer and a large shared
            embedding direction, chunks 0 and 3: greedy choices are decisive, so the literal
            free-running bar applies, and the head reads a residual that all the random layers
-           before it have written.
+           before it have written;
+  q4km  -- configs[4]: bench.py's Q4_K_M weights (ms_init_synthetic_q, seed 2; the block
+           generator restated in oracle/synth.py) at their EXACT fp32 dequantisation, chunks
+           0 and 5 (mode fp32 only).
 
 Three numerics modes of the oracle (oracle/llama_ref.py OracleLlama mode):
   fp32   -- un-rounded Llama (pinned against transformers on TINY): the parity target;
@@ -52,10 +55,10 @@ for p in (ROOT, PKG, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-MODEL = {"flat": (0, 0.02, 0.0), "sharp": (77, 0.02, 0.1)}  # seed, std, norm jitter
+MODEL = {"flat": (0, 0.02, 0.0), "sharp": (77, 0.02, 0.1), "q4km": (2, 0.02, 0.0)}  # seed, std, norm jitter
 P, GEN, TOPK = 2048, 128, 16
 SKETCH_SEED = 1234
-CHUNKS = {"flat": (0, 5), "sharp": (0, 3)}
+CHUNKS = {"flat": (0, 5), "sharp": (0, 3), "q4km": (0, 5)}
 
 
 def sketch_mats(H, V):
@@ -88,7 +91,7 @@ def topk(v, k=TOPK):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", choices=("flat", "sharp"), required=True)
+    ap.add_argument("--which", choices=("flat", "sharp", "q4km"), required=True)
     ap.add_argument("--mode", choices=("fp32", "f16", "engine"), required=True)
     ap.add_argument("--gen", type=int, default=GEN)
     ap.add_argument("--out", default=None)
@@ -100,7 +103,13 @@ def main():
     cfg = LLAMA32_3B
     t0 = time.time()
     SEED, STD, JIT = MODEL[args.which]
-    w = make_weights(cfg, SEED, std=STD, jitter=JIT)
+    if args.which == "q4km":
+        # configs[4]: bench.py's Q4_K_M model (ms_init_synthetic_q seed 2) at its EXACT fp32
+        # dequantisation (oracle/synth.py restates the device block generator bit for bit)
+        from oracle.synth import make_q4km_blocks, q4km_weights
+        w = q4km_weights(cfg, make_q4km_blocks(cfg, SEED, STD), SEED, JIT)
+    else:
+        w = make_weights(cfg, SEED, std=STD, jitter=JIT)
     meta = {"model": cfg.name, "n_layers": cfg.n_layers, "seed": SEED, "std": STD, "jitter": JIT,
             "mode": args.mode,
             "prompt_len": P, "gen": args.gen, "which": args.which, "chunks_doc": 0,

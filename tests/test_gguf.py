@@ -26,10 +26,17 @@ def write_gguf(path, meta: dict, tensors: list, align=32):
     out = bytearray(b"GGUF" + struct.pack("<IQQ", 3, len(tensors), len(meta)))
     for k, v in meta.items():
         out += _s(k)
-        if isinstance(v, str):
+        if isinstance(v, bool):
+            out += struct.pack("<IB", 7, int(v))
+        elif isinstance(v, str):
             out += struct.pack("<I", 8) + _s(v)
         elif isinstance(v, float):
             out += struct.pack("<If", 6, v)
+        elif isinstance(v, (list, tuple)):  # arrays: of strings (type 8) or of int32 (type 5)
+            if v and isinstance(v[0], str):
+                out += struct.pack("<IIQ", 9, 8, len(v)) + b"".join(_s(x) for x in v)
+            else:
+                out += struct.pack("<IIQ", 9, 5, len(v)) + b"".join(struct.pack("<i", int(x)) for x in v)
         else:
             out += struct.pack("<II", 4, v)
     off, datas = 0, []

@@ -20,7 +20,8 @@ def _bench():
     return b
 
 
-FIXTURES = [("flat", "fp32"), ("flat", "f16"), ("flat", "engine"), ("sharp", "fp32"), ("sharp", "engine")]
+FIXTURES = [("flat", "fp32"), ("flat", "f16"), ("flat", "engine"), ("sharp", "fp32"), ("sharp", "engine"),
+            ("q4km", "fp32")]
 
 
 @pytest.mark.parametrize("which,mode", FIXTURES)
@@ -32,6 +33,8 @@ def test_fixture_layout_and_prompts(which, mode):
     assert meta["n_layers"] == C.n_layers == 28 and meta["prompt_len"] == 2048
     if which == "flat":  # the bench's exact weights (bench.py init_synthetic(seed=0, std=0.02, norm_jitter=0))
         assert (meta["seed"], meta["std"], meta["jitter"]) == (0, 0.02, 0.0)
+    if which == "q4km":  # bench.py --weights q4_k_m: init_synthetic_q(seed=2, scale=0.02, norm_jitter=0)
+        assert (meta["seed"], meta["std"], meta["jitter"]) == (2, 0.02, 0.0)
     chunks = _bench().synthetic_chunks(8, 2048, doc=0, vocab=C.vocab, bos=C.bos_id)
     for ci in meta["chunks"]:
         k = f"c{ci}_"
@@ -65,3 +68,30 @@ def test_sharp_fixture_is_decisive_and_copies(mode):
     f = np.load(os.path.join(GOLD, "fullshape_flat_fp32.npz"))
     gap = f["c0_gen_top_vals"][:, 0] - f["c0_gen_top_vals"][:, 1]
     assert gap.min() < 0.01  # flat logits: near-ties exist
+
+
+def test_q4km_block_generator_matches_a_c_restatement():
+    """oracle/synth.py synth_qblocks (the fixture's weights) restates csrc/k_qgemv.hip
+    synth_qblocks_kernel: spot blocks of a Q4_K and a Q6_K tensor against hashes computed
+    once from a C restatement of the kernel body (clang, _Float16; values recorded here)."""
+    from oracle.synth import synth_qblocks
+
+    def h(r):
+        s = 0
+        for x in r:
+            s = (s * 131 + int(x)) % (1 << 64)
+        return s
+    got = [h(r) for r in synth_qblocks(12, 3, 2, 5, 3)] + [h(r) for r in synth_qblocks(14, 3, 2, 0, 0)]
+    assert got == [8019031135127078327, 9551836282545629676, 12036773794748307063,
+                   10111947276205690581, 16656358883380273260, 9763757120072924146]
+
+
+def test_q4km_fixture_is_exact_dequant():
+    """The Q4_K_M fixture's oracle ran on the EXACT fp32 dequantisation: the weights it
+    describes are not fp16-valued (the Q4_K d * q - m products need more than 11 bits)."""
+    from mapsum.config import LLAMA32_3B as C
+    from oracle.quants import dequant, q4_k_m_type
+    from oracle.synth import WO, synth_qblocks
+    qt = q4_k_m_type("wo", 0, C.n_layers)
+    w = dequant(synth_qblocks(qt, 64, 2, WO, 0, 0.02), qt)
+    assert np.any(w.astype(np.float16).astype(np.float32) != w)

@@ -80,9 +80,10 @@ def dev():
     return torch.device("cuda:0")
 
 
-def _engine(meta, which):
-    # the bench's engine geometry (bench.py: 8 slots, max_ctx = 2048 + 256): same split plans
-    e = Engine(CFG, device=0, max_batch=NCHUNK, max_ctx=meta["prompt_len"] + 256,
+def _engine(meta, which, max_batch=NCHUNK):
+    # the bench's engine geometry (bench.py: 8 slots, max_ctx = 2048 + 256): same split plans;
+    # other max_batch values select the engine's other decode regimes (test_gpu_golden28_regimes)
+    e = Engine(CFG, device=0, max_batch=max_batch, max_ctx=meta["prompt_len"] + 256,
                max_prefill_tokens=NCHUNK * meta["prompt_len"])
     e.init_synthetic(meta["seed"], meta["std"], meta["jitter"])
     if which == "sharp":

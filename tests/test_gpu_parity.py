@@ -1029,3 +1029,22 @@ def test_weight_regions_are_the_whole_model(dev, quant):
     finally:
         a.close()
         b.close()
+
+
+def test_wide_hidden_prefill_takes_the_plain_residual_path(dev):
+    """hidden / 128 > 24 (kGemmRsTiles): the prefill O / down residual epilogue would write
+    more statistics tiles than the ssq buffer holds, so the engine picks the plain residual add
+    + rmsnorm BEFORE launching.  A 2-layer model of hidden 4096 (32 q / 8 kv heads)
+    prefills and decodes against the oracle within the north star's 2e-2."""
+    cfg = TINY.with_(name="wide", hidden=4096, n_heads=32, n_kv_heads=8, ffn=1024)
+    oracle = OracleLlama(cfg, make_weights(cfg, SEED, std=0.03, jitter=JITTER))
+    ids = np.random.default_rng(11).integers(0, 4000, size=300).astype(np.int32)
+    with Engine(cfg, device=0, max_batch=2, max_ctx=512, max_prefill_tokens=1024) as e:
+        e.init_synthetic(SEED, 0.03, JITTER)
+        _, lg = e.forward(ids, hidden=False, logits=True)
+        ref, _ = oracle.forward(ids, all_logits=True)
+        err = rel(lg, ref)
+        print(f"hidden 4096 prefill logits rel err {err:.3e}")
+        assert err < 2e-2
+        got = e.generate([ids], num_predict=6, ignore_eos=True)[0].ids
+        assert len(got) == 6
