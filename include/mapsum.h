@@ -179,6 +179,11 @@ int ms_get_stats(const ms_engine* e, ms_stats* out);
 int ms_reset_stats(ms_engine* e);
 /* bit mask of kernel classes to bracket with HIP events (0 = off) */
 int ms_set_profiling(ms_engine* e, uint32_t class_mask);
+/* roctx ranges (rocprofv3 --marker-trace).  ms_step brackets itself ("mapsum.step") and its
+   phases ("mapsum.prefill", "mapsum.decode_run"); these let the host mark its own phases
+   (dist.gather_summaries: "mapsum.gather").  Nest; no-ops unless a profiler is attached. */
+int ms_trace_push(const char* name);
+int ms_trace_pop(void);
 int ms_synchronize(ms_engine* e);
 
 /* ---- parity probe (tests): one prompt through the prefill path -------------- */

@@ -30,6 +30,8 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "kernels.h"
 #include "mapsum.h"
 
@@ -38,6 +40,16 @@ using namespace ms;
 namespace {
 
 thread_local std::string g_last_error;
+
+// roctx ranges around the scheduler's phases (SURVEY.md §5 tracing): rocprofv3 --marker-trace
+// separates admission, the packed prefill and each decode run on the timeline (host ranges;
+// both phases end with a stream synchronisation, so they bracket the device work)
+struct TraceRange {
+  explicit TraceRange(const char* name) { roctxRangePushA(name); }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange&) = delete;
+  TraceRange& operator=(const TraceRange&) = delete;
+};
 
 struct MsError : std::runtime_error {
   int code;
@@ -130,6 +142,24 @@ struct ms_engine {
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
+  // decode attention with one page per wave (k_attn.hip v2, MS_ATTN_V2), attn_ppb waves / pages
+  // per block, fixed per engine like attn_ppw
+  bool attn_v2 = false;
+  int attn_ppb = 9;
+  // v2's splits merged inside the launch by the last block of each group (MS_ATTN_TICKET)
+  bool attn_ticket = false;
+  unsigned* attn_cnt = nullptr;  // [max_batch * Hk] arrival counters, zero between launches
+  bool attn2_ok(int B, int max_len) const {
+    return attn_v2 && slot_major && attn_decode2_supported(B, Hq, Hk, max_len, attn_ppb);
+  }
+  void attn_decode(const DecodeQKV& qa, const KVView& kv, const DecodeAttnArgs& da) {
+    prof_begin(K_ATTN_DECODE);
+    if (attn2_ok(da.B, da.max_len))
+      launch_attn_decode2(qa, attn, Hq, Hk, kv, da, attn_ws, attn_ppb, stream, attn_ticket ? attn_cnt : nullptr);
+    else
+      launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream);
+    prof_end(K_ATTN_DECODE);
+  }
   // Residual-fused decode (small-regime engines, fp16 O / down): O and down run unsplit on
   // resid_rt-row tiles (3072 / 12 = 256 workgroups, one per CU) and their epilogue adds into
   // the fp32 residual and emits the next projection's input itself -- xb = f16(x * g_next)
@@ -476,9 +506,7 @@ struct ms_engine {
       proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
       qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}};
     }
-    prof_begin(K_ATTN_DECODE);
-    launch_attn_decode(qa, attn, Hq, Hk, kv, da, attn_ws, stream);
-    prof_end(K_ATTN_DECODE);
+    attn_decode(qa, kv, da);
     resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm);
     const RowScale rs_ffn = cur_rs;
     const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
@@ -530,9 +558,7 @@ struct ms_engine {
     launch_rope_kv(qkv, T, Hq, Hk, tok_pos, tok_slot, cos_tab, sin_tab, kv, stream, decode || !pa.cos_tab);
     prof_end(K_MISC);
     if (decode) {
-      prof_begin(K_ATTN_DECODE);
-      launch_attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}}, attn, Hq, Hk, kv, da, attn_ws, stream);
-      prof_end(K_ATTN_DECODE);
+      attn_decode(DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}}, kv, da);
     } else {
       prof_begin(K_ATTN_PREFILL);
       launch_attn_prefill(qkv, attn, Hq, Hk, kv, pa, stream);
@@ -794,7 +820,15 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     const int shapes[5][2] = {{E.QKVN, E.H}, {E.H, E.Hq * E.D}, {2 * E.F, E.H}, {E.H, E.F}, {E.V, E.H}};
     for (auto& sh : shapes) gws = std::max(gws, gemv_workspace_bytes(Md, sh[0], sh[1]));
     E.gemv_ws = E.dalloc<char>(gws, true);
-    E.attn_ws = (float*)E.dalloc<char>(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
+    // decode attention: v2 (one page per wave) for engines of <= 16 slots (MS_ATTN_V2 overrides)
+    E.attn_ppb = attn_decode2_ppb(cfg->max_batch, E.Hk, cfg->max_ctx);
+    E.attn_v2 = cfg->max_batch <= 16;
+    if (const char* v = getenv("MS_ATTN_V2")) E.attn_v2 = atoi(v) != 0;
+    if (const char* v = getenv("MS_ATTN_TICKET")) E.attn_ticket = atoi(v) != 0;
+    E.attn_cnt = E.dalloc<unsigned>((size_t)cfg->max_batch * E.Hk, true);
+    E.attn_ws = (float*)E.dalloc<char>(std::max(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
+                                                attn_decode2_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx,
+                                                                             E.attn_ppb)),
                                        true);
     E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * std::min(std::max(cfg->max_batch, 64), 256) *
                               std::max(E.QKVN, E.H));
@@ -1496,6 +1530,7 @@ int ms_step(ms_engine* e) {
     HIP_OK(hipSetDevice(E.cfg.device));
     // Profiling runs serialise the phases, so every bracketed launch runs alone on the chip.
     const bool ov = E.overlap && E.prof_mask == 0;
+    TraceRange tr_step("mapsum.step");
     // 1. admit (the new slots' block-table rows go out on the prefill stream)
     E.use(E.cp);
     std::vector<Seq*> admitted;
@@ -1529,6 +1564,7 @@ int ms_step(ms_engine* e) {
       }
     };
     if (!admitted.empty()) {
+      TraceRange tr("mapsum.prefill");
       HIP_OK(hipEventRecord(E.cp.ev_a, E.cp.stream));
       prefill(E, admitted, E.L, nullptr, &first);
       HIP_OK(hipEventRecord(E.cp.ev_b, E.cp.stream));
@@ -1561,7 +1597,10 @@ int ms_step(ms_engine* e) {
       }
       k = std::max(1, std::min(k, ((max_len + 255) / 256) * 256 - max_len + 1));
       std::vector<int32_t> ids;
-      decode_run(E, sub, k, ids);  // records ev_a/ev_b around its device work and syncs
+      {
+        TraceRange tr("mapsum.decode_run");
+        decode_run(E, sub, k, ids);  // records ev_a/ev_b around its device work and syncs
+      }
       float ms_ = 0.f;
       HIP_OK(hipEventElapsedTime(&ms_, E.ev_a, E.ev_b));
       E.stats.decode_ms += ms_;
@@ -1614,6 +1653,17 @@ int ms_poll(ms_engine* e, ms_result* out, int32_t cap) {
     E.done.erase(E.done.begin(), E.done.begin() + n);
     return n;
   });
+}
+
+int ms_trace_push(const char* name) {
+  if (!name) return MS_EINVAL;
+  roctxRangePushA(name);
+  return MS_OK;
+}
+
+int ms_trace_pop(void) {
+  roctxRangePop();
+  return MS_OK;
 }
 
 int ms_get_stats(const ms_engine* e, ms_stats* out) {

@@ -751,3 +751,382 @@ void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView 
 }
 
 }  // namespace ms
+
+namespace ms {
+
+// ============================================================ decode, one page per wave (v2)
+// For the small-batch regime (engines of <= 16 slots, the configs[1] bench at B = 8) the
+// kernel above is latency-bound: each wave walks 2 pages and issues the second page only after
+// the first has landed and been multiplied, and the block prologue (the QKV slab fold) waits
+// for the first page (vmcnt retires in issue order).  Here every wave owns ONE page and issues
+// it at once -- K into registers, V by LDS DMA straight into its V^T image (v_swz layout,
+// applied on the DMA source) -- so a block's whole page range (ppb pages, 32 KB each) is in
+// flight from its first microsecond and the chip requests all of a step's K/V in one burst.
+// One block of ppb waves per (sequence, kv head, split) with ppb fixed per ENGINE (the split
+// boundaries, multiples of ppb pages, set a sequence's summation order: batch invariance) and
+// chosen so a full batch is ~one block per CU; the splits of one (sequence, kv head) share
+// blockIdx % 8 (one XCD: their partials meet in one L2).  Waves merge (m, l, O^T) in LDS in
+// wave order; the block writes the split's partial (attn_decode_combine_kernel merges them in
+// split order) or, with a single split, the fp16 output itself.  Arithmetic per page is the
+// kernel above's (same MFMA orientation, fp16 P, lazy-free online softmax per page).
+constexpr int kPpbMin = 4, kPpbMax = 9;  // 9 x 16 KB V images + the prologue fit 160 KB of LDS
+
+// a barrier for LDS written by ds_write only: waits lgkmcnt, not vmcnt (the pages' loads and the
+// V DMA stay in flight across it; gemv_common.h lds_sync)
+__device__ __forceinline__ void attn2_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+int attn_decode2_ppb(int max_batch, int Hk, int max_ctx) {
+  const char* ev = getenv("MS_ATTN_PPB");  // read per engine (tests pin several values in one process)
+  const int env = ev ? atoi(ev) : 0;
+  if (env > 0) return std::max(kPpbMin, std::min(env, kPpbMax));
+  const long np = (max_ctx + kPage - 1) / kPage;
+  const long want = (np * max_batch * Hk + 255) / 256;  // ~one block per CU at a full batch
+  return (int)std::max((long)kPpbMin, std::min((long)kPpbMax, want));
+}
+
+static size_t attn2_lds_bytes(int ppb, int G) {
+  return (size_t)ppb * 16384 + (size_t)(G + 2) * kHeadDim * 4 + (size_t)(G + 2) * kHeadDim * 2;
+}
+
+bool attn_decode2_supported(int B, int Hq, int Hk, int max_len, int ppb) {
+  (void)B;
+  if (Hk < 1 || Hq % Hk || Hq / Hk > kMaxGroup || ppb < kPpbMin || ppb > kPpbMax) return false;
+  const int np = (max_len + kPage - 1) / kPage;
+  return (np + ppb - 1) / ppb <= kMaxSplits && attn2_lds_bytes(ppb, Hq / Hk) <= 160 * 1024;
+}
+
+size_t attn_decode2_workspace_bytes(int B, int Hq, int max_len, int ppb) {
+  const int np = (max_len + kPage - 1) / kPage;
+  return (size_t)B * Hq * ((np + ppb - 1) / ppb) * 132 * sizeof(float);
+}
+
+// loads the compiler cannot see (vmcnt retires in issue order, and the compiler's own waits
+// only count the loads it sees): the prologue's small L2-resident operands are issued first
+// through these, then the page's V DMA and K loads, and ONE manual s_waitcnt vmcnt(32) -- the
+// page's 16 + 16 still in flight -- covers them, so the prologue runs while the page streams
+__device__ __forceinline__ float ld_f32_opaque(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// TICKET: the splits of one (sequence, kv head) are merged inside the launch by the block that
+// finishes last (an agent-scope arrival counter per group, cnt[B * Hk], zero between launches:
+// the last arriver resets it), with attn_decode_combine_kernel's arithmetic in split order --
+// the same bits as the second launch; the group's blocks share one XCD (blockIdx % 8), so the
+// partials and the counter meet in one L2
+template <bool FROM_SLABS, int PPB, bool TICKET>
+__global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
+                                                                DecodeAttnArgs a, float* __restrict__ ws,
+                                                                f16_t* __restrict__ out, int nsplit,
+                                                                float scale_log2, unsigned* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NTHR = 64 * PPB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int BH = a.B * Hk;
+  const int split = blockIdx.x / BH, grp = blockIdx.x - split * BH;
+  const int b = grp / Hk, kvh = grp - b * Hk;
+  const int G = Hq / Hk;
+  const int len = a.seq_len[b];
+  const int slot = a.seq_slot[b];
+  const int np = (len + kPage - 1) / kPage;
+  const int pg = split * PPB + wave;  // this wave's page (none when >= np)
+  const int pos = len - 1;            // the new token
+  const int row_stride = (Hq + 2 * Hk) * kHeadDim;
+  char* vs_ = smem + wave * 16384;
+  float* raw = (float*)(smem + (size_t)PPB * 16384);  // [(G+2)][128] fp16-rounded sums
+  f16_t* qn = (f16_t*)(raw + (G + 2) * kHeadDim);     // [G][128] roped q
+  f16_t* kn = qn + G * kHeadDim;                       // [128] roped k of the new token
+  f16_t* vn = kn + kHeadDim;                           // [128] v of the new token
+  const bool has_page = pg < np;                       // wave-uniform
+  // slot-major pool (launch_attn_decode2 checks): page ids are arithmetic, no table load
+  const size_t pbase = (((size_t)slot * kv.max_pages + pg) * kv.n_kv_heads + kvh) * kPage * kHeadDim;
+
+  // 0. the prologue's operands: the row's deferred-norm partial sums, the QKV slab values and
+  // this thread's rope pair (opaque loads, issued first)
+  const bool owns_new = (pos / kPage) / PPB == split;  // block-uniform
+  const int nvec = FROM_SLABS ? (G + (owns_new ? 2 : 0)) * kHeadDim : 0;
+  constexpr int PER = ((kMaxGroup + 2) * kHeadDim + NTHR - 1) / NTHR;
+  float rv[4] = {0.f, 0.f, 0.f, 0.f};
+  float sv[PER][kMaxSlabs];
+  float rcs = 0.f, rsn = 0.f;
+  if constexpr (FROM_SLABS) {
+    if (qa.rs.ssq) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int t = lane + 64 * i;
+        if (64 * i < qa.rs.tiles) rv[i] = ld_f32_opaque(qa.rs.ssq + (size_t)min(t, qa.rs.tiles - 1) * a.B + b);
+      }
+    }
+    const size_t sstride = (size_t)a.B * row_stride;
+    const float* src = qa.slabs + (size_t)b * row_stride;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (i * NTHR < nvec) {  // block-uniform
+        const int e = min(tid + i * NTHR, nvec - 1);
+        const int hh = e >> 7, j = e & 127;  // hh < G: q head kvh*G+hh; G: k; G+1: v
+        const int col = hh < G ? (kvh * G + hh) * kHeadDim + j
+                               : (hh == G ? (Hq + kvh) * kHeadDim + j : (Hq + Hk + kvh) * kHeadDim + j);
+#pragma unroll
+        for (int q = 0; q < kMaxSlabs; ++q)
+          if (q < qa.S) sv[i][q] = ld_f32_opaque(src + q * sstride + col);
+      }
+    }
+    rcs = ld_f32_opaque(qa.cos_tab + (size_t)pos * 64 + (tid & 63));
+    rsn = ld_f32_opaque(qa.sin_tab + (size_t)pos * 64 + (tid & 63));
+  }
+  // 1. this wave's page: V by LDS DMA into its V^T image (chunk c of row rr lands at
+  // v_swz(rr, c): lane l of 1-KiB piece i covers row 4i + l / 16, LDS chunk l % 16, so it loads
+  // the global chunk (l % 16) ^ ((row & 7) << 1)), then K into registers (16 rows x 64 B per
+  // instruction, as the kernel above)
+  u32x4 kf[4][4];
+  if (has_page) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rr = 4 * i + (lane >> 4), ch = (lane & 15) ^ ((rr & 7) << 1);
+      dma16_opaque(kv.v + pbase + rr * kHeadDim + ch * 8, vs_ + i * 1024);
+    }
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+        kf[mt][s4] = ld_stream(kv.k + pbase + (mt * 16 + r) * kHeadDim + 32 * s4 + 8 * g);
+  }
+
+  // 2. prologue: fold the slabs, the row scale, RoPE -> qn / kn / vn; the owner writes the new
+  // token's K/V into the cache (rope_kv_kernel's arithmetic, as the kernel above)
+  if constexpr (FROM_SLABS) {
+    // the opaque loads above have landed once at most the page's 32 are in flight
+    if (has_page) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(rv[i]));
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+      for (int q = 0; q < kMaxSlabs; ++q) asm volatile("" : "+v"(sv[i][q]));
+    asm volatile("" : "+v"(rcs), "+v"(rsn));
+    float rsum = 0.f;
+    if (qa.rs.ssq) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (!(lane + 64 * i < qa.rs.tiles)) rv[i] = 0.f;
+      rsum = ((rv[0] + rv[1]) + rv[2]) + rv[3];
+    }
+    const float rrow = qa.rs.ssq ? rs_rinv(wave_sum(rsum), qa.rs) : 1.0f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = tid + i * NTHR;
+      if (i * NTHR >= nvec) break;
+      float acc = sv[i][0];
+#pragma unroll
+      for (int q = 1; q < kMaxSlabs; ++q)
+        if (q < qa.S) acc += sv[i][q];
+      if (e < nvec) raw[e] = h2f(f2h(acc * rrow));
+    }
+    attn2_lds_sync();
+    const int nrot = (G + (owns_new ? 1 : 0)) * 64;  // (head, i) pairs: the q heads, then k
+    for (int e = tid; e < nrot; e += NTHR) {
+      const int hh = e >> 6, i = e & 63;  // i == tid & 63 (NTHR % 64 == 0)
+      const float lo = raw[hh * kHeadDim + rope_perm(i)], hi = raw[hh * kHeadDim + rope_perm(64 + i)];
+      const float ra = __fsub_rn(__fmul_rn(lo, rcs), __fmul_rn(hi, rsn));
+      const float rb = __fadd_rn(__fmul_rn(hi, rcs), __fmul_rn(lo, rsn));
+      f16_t* dst = hh < G ? qn + hh * kHeadDim : kn;
+      dst[i] = f2h(ra);
+      dst[64 + i] = f2h(rb);
+    }
+    if (owns_new && tid < kHeadDim) vn[tid] = f2h(raw[(G + 1) * kHeadDim + tid]);
+    attn2_lds_sync();
+    if (owns_new && tid < kHeadDim) {
+      const size_t o = ((((size_t)slot * kv.max_pages + pos / kPage) * kv.n_kv_heads + kvh) * kPage + pos % kPage) *
+                           kHeadDim + tid;
+      kv.k[o] = kn[tid];
+      kv.v[o] = vn[tid];
+    }
+  }
+
+  // 3. S^T = K Q^T, softmax over the page, O^T = V^T P^T
+  f32x4 o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  if (has_page) {
+    f16x8 qf[4];
+    const int hl = min(r, G - 1);
+    if constexpr (FROM_SLABS) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const f16x8*)(qn + hl * kHeadDim + 32 * s4 + 8 * g);
+    } else {
+      const f16_t* qrow = qa.qkv + (size_t)b * row_stride + (kvh * G + hl) * kHeadDim;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) qf[s4] = as_f16x8(*(const uint4*)(qrow + 32 * s4 + 8 * g));
+    }
+    const int off = pos % kPage;
+    const bool patch = FROM_SLABS && pg == pos / kPage;  // wave-uniform: holds the new token
+    if (patch) {
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+          if (mt * 16 + r == off) kf[mt][s4] = *(const u32x4*)(kn + 32 * s4 + 8 * g);
+    }
+    f32x4 sc[4];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      sc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) sc[mt] = mfma16(__builtin_bit_cast(f16x8, kf[mt][s4]), qf[s4], sc[mt]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = pg * kPage + mt * 16 + 4 * g + j;
+        const float v = (key >= len) ? -INFINITY : sc[mt][j] * scale_log2;
+        sc[mt][j] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = grp_max(mx);  // finite: key pg*64 < len is always visible
+    float rs = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = (sc[mt][j] == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(sc[mt][j] - mx);
+        sc[mt][j] = p;
+        rs += p;
+      }
+    l_run = grp_sum(rs);
+    m_run = mx;
+    // the V image has landed (its DMA was issued before the K loads the S MFMAs waited for)
+    wait_vmcnt0();
+    // rows past the sequence (last page) zeroed -- no stale V in P.V -- and the new token's row
+    if (pg == np - 1) {
+      const int first = len - pg * kPage;  // rows [first, 64) are past the sequence
+      for (int e = first * 16 + lane; e < 64 * 16; e += 64)
+        *(u32x4*)(vs_ + v_swz(e >> 4, e & 15)) = u32x4{0, 0, 0, 0};
+    }
+    if (patch && lane < 16) *(u32x4*)(vs_ + v_swz(off, lane)) = *(const u32x4*)(vn + lane * 8);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the patched rows are in LDS
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int kstep = 0; kstep < 2; ++kstep) {
+      const f16x8 pf = pack_p(sc[2 * kstep], sc[2 * kstep + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        const f16x8 vt = load_vt(vs_, dt, kstep, lane);
+        o[dt] = mfma16(vt, pf, o[dt]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+  }
+  // 4. publish (m, l, O^T) of this wave's 16 columns into its own LDS region, merge in wave order
+  {
+    float* mw = (float*)vs_;
+    if (g == 0) { mw[r * 130 + 0] = m_run; mw[r * 130 + 1] = l_run; }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mw[r * 130 + 2 + dt * 16 + 4 * g + j] = o[dt][j];
+  }
+  __syncthreads();
+  for (int idx = tid; idx < G * 130; idx += NTHR) {
+    const int c = idx / 130, k = idx - c * 130;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < PPB; ++w) M = fmaxf(M, ((const float*)(smem + w * 16384))[c * 130]);
+    float acc = 0.f, L = 0.f;
+#pragma unroll
+    for (int w = 0; w < PPB; ++w) {
+      const float* mw = (const float*)(smem + w * 16384);
+      const float m_w = mw[c * 130];
+      const float f = (m_w == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(m_w - M);
+      acc += (k == 0) ? 0.f : f * mw[c * 130 + k];
+      L += f * mw[c * 130 + 1];
+    }
+    if (nsplit == 1) {
+      // a single split: O / L straight to the output (the combine's arithmetic with one
+      // partial, whose weight 2^(M - M) is 1)
+      if (k >= 2) out[(size_t)b * Hq * kHeadDim + (kvh * G + c) * kHeadDim + (k - 2)] = f2h(acc / L);
+    } else if constexpr (TICKET) {
+      // write-through (sc1) partial stores: the hand-off needs no release fence (an agent-scope
+      // fence writes back and invalidates the L2 -- 64 us per launch, measured)
+      __hip_atomic_store(ws + (((size_t)b * Hq + kvh * G + c) * nsplit + split) * 132 + k, (k == 0) ? M : acc,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      ws[(((size_t)b * Hq + kvh * G + c) * nsplit + split) * 132 + k] = (k == 0) ? M : acc;
+    }
+  }
+  if constexpr (TICKET) {
+    if (nsplit == 1) return;
+    __shared__ unsigned last_s;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores are done
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last_s = old == (unsigned)(nsplit - 1);
+    }
+    __syncthreads();
+    if (!last_s) return;
+    // the last block of the group: every split's partial, by sc1 loads (no stale cached copy),
+    // merged as attn_decode_combine_kernel does (same order, same bits)
+    auto ld = [](const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (int idx = tid; idx < G * kHeadDim; idx += NTHR) {
+      const int c = idx >> 7, d = idx & 127;
+      const float* p = ws + ((size_t)b * Hq + kvh * G + c) * nsplit * 132;
+      float M = -INFINITY;
+      for (int q = 0; q < nsplit; ++q) M = fmaxf(M, ld(p + q * 132));
+      float L = 0.f, O = 0.f;
+      for (int q = 0; q < nsplit; ++q) {
+        const float m_q = ld(p + q * 132);
+        const float f = m_q == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_q - M);
+        L += f * ld(p + q * 132 + 1);
+        O += f * ld(p + q * 132 + 2 + d);
+      }
+      out[(size_t)b * Hq * kHeadDim + (kvh * G + c) * kHeadDim + d] = f2h(O / L);
+    }
+    if (tid == 0) __hip_atomic_store(cnt + grp, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv, DecodeAttnArgs a,
+                         float* ws, int ppb, hipStream_t s, unsigned* cnt) {
+  if (a.B <= 0) return;
+  if (!attn_decode2_supported(a.B, Hq, Hk, a.max_len, ppb) || !kv.slot_major) return;  // callers check
+  if (qa.slabs && (qa.S < 1 || qa.S > kMaxSlabs)) return;
+  if (qa.slabs && qa.rs.ssq && (qa.rs.tiles < 1 || qa.rs.tiles > 256)) return;
+  const int np = (a.max_len + kPage - 1) / kPage;
+  const int nsplit = (np + ppb - 1) / ppb;
+  const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
+  const dim3 grid(a.B * Hk * nsplit);
+  const size_t lds = attn2_lds_bytes(ppb, Hq / Hk);
+#define A2(P_)                                                                                                \
+  case P_:                                                                                                    \
+    if (qa.slabs && cnt)                                                                                      \
+      MS_LAUNCH((attn_decode2_kernel<true, P_, true>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,    \
+                out, nsplit, scale_log2, cnt);                                                                \
+    else if (qa.slabs)                                                                                        \
+      MS_LAUNCH((attn_decode2_kernel<true, P_, false>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,   \
+                out, nsplit, scale_log2, cnt);                                                                \
+    else                                                                                                      \
+      MS_LAUNCH((attn_decode2_kernel<false, P_, false>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,  \
+                out, nsplit, scale_log2, cnt);                                                                \
+    break;
+  switch (ppb) {
+    A2(4) A2(5) A2(6) A2(7) A2(8) A2(9)
+    default: return;
+  }
+#undef A2
+  if (nsplit > 1 && !(qa.slabs && cnt))
+    MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
+}
+
+}  // namespace ms

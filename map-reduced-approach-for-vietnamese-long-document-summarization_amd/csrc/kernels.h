@@ -253,6 +253,15 @@ bool attn_decode_supported(int B, int Hq, int Hk, int max_len);
 int attn_decode_ppw(int max_batch, int Hk, int max_ctx);
 void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv,
                         DecodeAttnArgs a, float* ws, hipStream_t s);
+// one page per wave, ppb waves per block (k_attn.hip "v2"): pages per block fixed per engine
+// from its max_batch / max_ctx (the split boundaries set a sequence's summation order)
+int attn_decode2_ppb(int max_batch, int Hk, int max_ctx);
+bool attn_decode2_supported(int B, int Hq, int Hk, int max_len, int ppb);
+size_t attn_decode2_workspace_bytes(int B, int Hq, int max_len, int ppb);
+// cnt (optional, [B * Hk] zeroed unsigned): merge the splits inside the launch (the last block of
+// each (sequence, kv head) combines, bit-identical to the second launch); null: combine kernel
+void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv, DecodeAttnArgs a,
+                         float* ws, int ppb, hipStream_t s, unsigned* cnt = nullptr);
 
 // synthetic weights (oracle/synth.py restates this generator)
 // row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the

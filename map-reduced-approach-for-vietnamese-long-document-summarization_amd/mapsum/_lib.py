@@ -35,6 +35,7 @@ EXPORTED = (
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
     "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
+    "ms_trace_push", "ms_trace_pop",
 )
 
 
@@ -122,6 +123,8 @@ def load() -> C.CDLL:
         "ms_weight_regions": (i32, [vp, C.POINTER(vp), C.POINTER(i64), i32]),
         "ms_quant_manifest": (i32, [vp, pi32, i32]),
         "ms_declare_weight_q": (i32, [vp, i32, i32, i32]),
+        "ms_trace_push": (i32, [C.c_char_p]),
+        "ms_trace_pop": (i32, []),
     }
     ab = bool(os.environ.get("MAPSUM_LIB"))  # an A/B build may predate the newest op hooks
     for name, (res, args) in sig.items():
@@ -141,3 +144,28 @@ def check(rc: int, handle=None, what: str = "") -> int:
         msg = load().ms_last_error(handle)
         raise RuntimeError(f"libmapsum {what} failed ({rc}): {msg.decode() if msg else ''}")
     return rc
+
+
+class trace:
+    """``with trace("mapsum.gather"):`` -- a roctx range (ms_trace_push / ms_trace_pop) around a
+    host phase, shown by rocprofv3 --marker-trace next to the engine's own ranges; a no-op when
+    libmapsum cannot be loaded (CPU-only tests of the host code)."""
+
+    def __init__(self, name: str):
+        self.name = name.encode()
+        self.lib = None
+
+    def __enter__(self):
+        try:
+            lib = load()
+            if hasattr(lib, "ms_trace_push"):
+                lib.ms_trace_push(self.name)
+                self.lib = lib
+        except (OSError, RuntimeError):
+            self.lib = None
+        return self
+
+    def __exit__(self, *exc):
+        if self.lib is not None:
+            self.lib.ms_trace_pop()
+        return False

@@ -76,8 +76,10 @@ def gather_summaries(packed: np.ndarray, max_rows: int, device=None, group=None)
     if device is not None:
         t = t.to(device)
     outs = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(outs, t, group=group)
-    return torch.cat(outs).cpu().numpy()
+    from ._lib import trace
+    with trace("mapsum.gather"):
+        dist.all_gather(outs, t, group=group)
+        return torch.cat(outs).cpu().numpy()
 
 
 def env_rank() -> tuple[int, int, int]:

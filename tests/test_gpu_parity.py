@@ -709,6 +709,42 @@ def test_decode_attention_variants(oracle, monkeypatch, slabs, resid):
         e.close()
 
 
+_ATTN2 = {}
+
+
+@pytest.mark.parametrize("v2,ticket,ppb", [(0, 0, 0), (1, 0, 4), (1, 1, 4), (1, 0, 9), (1, 1, 9)])
+def test_decode_attention_v2(oracle, monkeypatch, v2, ticket, ppb):
+    """Decode attention with one KV page per wave (k_attn.hip v2: ppb pages per block, the
+    splits merged by the combine launch or, TICKET, by the last block of each group inside the
+    launch) against the oracle over prompts of 1..12 pages (1..3 splits); the in-launch merge
+    is bit-identical to the combine launch (same arithmetic, same split order), and the ids do
+    not depend on the batch's composition."""
+    monkeypatch.setenv("MS_ATTN_V2", str(v2))
+    monkeypatch.setenv("MS_ATTN_TICKET", str(ticket))
+    if ppb:
+        monkeypatch.setenv("MS_ATTN_PPB", str(ppb))
+    e = Engine(TINY, device=0, max_batch=6, max_ctx=1024, max_prefill_tokens=4096)
+    try:
+        e.init_synthetic(SEED, STD, JITTER)
+        prompts = [_prompt(n, 40 + n) for n in (3, 61, 64, 65, 300, 700)]
+        res = e.generate(prompts, num_predict=24, ignore_eos=True)
+        agree = total = 0
+        for p, r in zip(prompts, res):
+            a, flips = _teacher_forced_agreement(oracle, p, r.ids)
+            agree += a
+            total += len(r.ids)
+            for pos, gap, top in flips:
+                assert gap <= 1e-2 * (abs(top) + 1.0), (pos, gap, top)
+        assert agree / total >= 0.95, (agree, total)
+        alone = e.generate(prompts[4:5], num_predict=24, ignore_eos=True)[0]
+        assert alone.ids == res[4].ids
+        _ATTN2[(v2, ticket, ppb)] = [r.ids for r in res]
+        if ticket and (v2, 0, ppb) in _ATTN2:
+            assert _ATTN2[(v2, ticket, ppb)] == _ATTN2[(v2, 0, ppb)]
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("nb", [20, 50, 70, 130])
 def test_decode_paths_larger_batch(oracle, nb):
     """B = 20 runs the weight-streaming GEMVs with MT = 2 tiles; B >= 24 the large-batch
