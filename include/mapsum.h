@@ -217,7 +217,7 @@ int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t*
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* stream);
 /* prefill O / down with the residual update fused (the engine's prefill layer): x fp32 [M][N] +=
-   A . W^T, and the input of the next normalised projection: xg_out fp16 [M][N] = f16(x * gamma),
+   A . W^T, and the input of the next normalised projection: xg_out fp16 [M][N] = f16(x * gamma * 2^-4),
    ssq_out fp32 [tiles][M] = per-128-column sums of the new x^2 (tiles = ms_gemm_resid_tiles(M, N) = N / 128),
    the deferred RMSNorm statistics the next ms_op_gemm takes through ms_op_set_row_scale */
 int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const void* gamma, float* ssq_out,
@@ -241,13 +241,14 @@ int ms_op_gemv_strided(const void* X, const void* W, void* out, int32_t M, int32
                        int32_t ldk, int32_t ldo, int32_t epilogue, void* stream);
 /* decode O / down with the residual update fused (the engine's small-regime layer): x fp32
    [M][N] += X . W^T on rt-row tiles (N % rt == 0, tiles = N / rt <= 256), and the input of the
-   next normalised projection: xg_out fp16 [M][N] = f16(x * gamma), ssq_out fp32 [tiles][M] =
+   next normalised projection: xg_out fp16 [M][N] = f16(x * gamma * 2^-4), ssq_out fp32 [tiles][M] =
    per-tile sums of the new x^2 (its deferred RMSNorm statistics, see ms_op_set_row_scale) */
 int ms_op_gemv_resid(const void* X, const void* W, float* x, void* xg_out, const void* gamma,
                      float* ssq_out, int32_t M, int32_t N, int32_t K, int32_t rt, void* stream);
 /* the deferred RMSNorm of the numerics contract: the next ms_op_gemm /
    ms_op_gemv / ms_op_gemv_split / ms_op_dgemm / ms_op_qgemv / ms_op_qgemv_split calls of the
-   calling thread scale output row r by 1/sqrt(sum_t ssq[t][r] / hidden + eps) (ssq [tiles][M];
+   calling thread scale output row r by 16/sqrt(sum_t ssq[t][r] / hidden + eps) -- 16 undoes the
+   2^-4 the producers pre-scale their fp16 output by (ssq [tiles][M];
    gemm / dgemm: tiles == 1); ssq = NULL turns the scale off.  Test hook: the engine passes the
    scale with each launch. */
 int ms_op_set_row_scale(const float* ssq, int32_t tiles, int32_t hidden, float eps);
@@ -261,7 +262,7 @@ int ms_op_dgemm(const void* X, const void* W, void* out, int32_t M, int32_t N, i
 int ms_op_gemv_split(const void* X, const void* W, float* slabs, int32_t M, int32_t N, int32_t K,
                      int32_t S, int32_t waves, void* stream);
 /* x fp32 [rows][hidden] += slab_0 + ... + slab_{S-1} (slab order); then the input of the
-   normalised projection that follows: y fp16 = f16(x * w), ssq[r] = sum of x[r]^2 (one tile) */
+   normalised projection that follows: y fp16 = f16(x * w * 2^-4), ssq[r] = sum of x[r]^2 (one tile) */
 int ms_op_residual_rmsnorm(float* x, const float* slabs, int32_t S, const void* w, void* y, float* ssq,
                            int32_t rows, int32_t hidden, void* stream);
 /* K-quant ops: raw ggml blocks -> fp32 (bit-exact restatement of llama.cpp's
@@ -276,9 +277,10 @@ int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void*
    (the quantised counterpart of ms_op_gemv_split; K % (256*S) == 0) */
 int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows, float* slabs,
                       int32_t M, int32_t N, int32_t K, int32_t S, void* stream);
-/* the input of a normalised projection: y fp16 [rows][hidden] = f16(x * w) and ssq[r] = sum
+/* the input of a normalised projection: y fp16 [rows][hidden] = f16(x * w * 2^-4) and ssq[r] = sum
    of x[r]^2 over x fp32 [.][hidden] rows (row_idx optional gather); the projection then scales
-   its output rows by 1/sqrt(ssq / hidden + eps) (ms_op_set_row_scale) */
+   its output rows by 16/sqrt(ssq / hidden + eps) (ms_op_set_row_scale).  The 2^-4 pre-scale
+   (exact) keeps un-normalised residual rows up to ~1e6 inside fp16 (kernels.h kXgScale). */
 int ms_op_rmsnorm(const void* x, const void* w, void* y, float* ssq, int32_t rows, int32_t hidden,
                   const int32_t* row_idx, void* stream);
 /* ids[r] = argmax_j logits[r][j] (ties -> lowest j; -1 when no logit of the row is finite) */

@@ -407,11 +407,14 @@ struct ms_engine {
   int proj_split(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
                  const RowScale* rs) {
     if (row_groups(M)) {
-      int used = 1;
+      // every group must write the same number of slabs: the fold adds S slabs for all rows
+      int used = 0;
       for (int r0 = 0; r0 < M; r0 += kMaxGemvRows) {
         const RowScale g = rs ? rs_rows(*rs, r0) : RowScale{};
-        used = proj_split_rows(q, X + (size_t)r0 * K, W, std::min(M - r0, (int)kMaxGemvRows), N, K, S, Sl,
-                               rs ? &g : nullptr, slabs + (size_t)r0 * N, M);
+        const int u = proj_split_rows(q, X + (size_t)r0 * K, W, std::min(M - r0, (int)kMaxGemvRows), N, K, S, Sl,
+                                      rs ? &g : nullptr, slabs + (size_t)r0 * N, M);
+        REQUIRE(used == 0 || u == used, MS_EIO, "row groups split a projection differently");
+        used = u;
       }
       return used;
     }

@@ -8,15 +8,9 @@ __device__ __forceinline__ uint4 ldg16(const void* p) { return *(const uint4*)p;
 
 // once-read decode weight streams: plain loads (non-temporal ones measured slower on the whole
 // decode step, 2.45 vs 2.29 ms, profiles/r01 v5_nt_stream_ab_rejected)
-#ifndef MS_NT_WEIGHTS
+// (re-measured round 5 on the current GEMVs: nt weight loads 2.30 vs 2.10 ms per decode step,
+// profiles/r05/v4_attn_ticket_nt_ab3.txt)
 __device__ __forceinline__ uint4 ldw16(const void* p) { return *(const uint4*)p; }
-#else  // A/B build (round 5): nt weight loads, make EXTRA=-DMS_NT_WEIGHTS
-__device__ __forceinline__ uint4 ldw16(const void* p) {
-  typedef uint32_t u4nt __attribute__((ext_vector_type(4)));
-  const u4nt v = __builtin_nontemporal_load((const u4nt*)p);
-  return uint4{v[0], v[1], v[2], v[3]};
-}
-#endif
 
 // s_waitcnt immediate for vmcnt(n) with expcnt/lgkmcnt left alone (gfx9 encoding)
 __host__ __device__ constexpr int vmcnt_imm(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
@@ -306,7 +300,7 @@ __device__ __forceinline__ void gemv_epilogue(const float* red, const float* rin
         // v_cvt_pk_f16_f32): left visible, the compiler fused x * g -> fp16 into one
         // v_fma_mixlo_f16, a single rounding of the exact product that differs at ties
         if (ga.xg_out) {
-          float xg = xo * (ELEMS <= 256 ? pre.g : h2f(ga.gamma[col]));
+          float xg = xo * (ELEMS <= 256 ? pre.g : h2f(ga.gamma[col])) * kXgScale;
           asm volatile("" : "+v"(xg));
           ga.xg_out[(size_t)row * ldo + col] = f2h(xg);
         }

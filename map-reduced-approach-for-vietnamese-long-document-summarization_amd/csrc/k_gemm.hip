@@ -71,7 +71,7 @@ __device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, 
 }
 // ---- the residual epilogue's outputs for the next normalised projection
 __device__ __forceinline__ void gemm_resid_xg(const GemmResid& gr, size_t o, float v, float g, float& ss) {
-  float p = v * g;
+  float p = v * g * kXgScale;  // (kernels.h: the GEMM input pre-scaled by 2^-4, exactly)
   asm volatile("" : "+v"(p));  // the fp32 product, then one fp16 rounding (no v_fma_mixlo_f16)
   gr.xg[o] = f2h(p);
   ss += v * v;

@@ -268,13 +268,14 @@ static void gemv_dispatch(const f16_t* X, const f16_t* W, void* out, int M, int 
   const int rt = ga_in ? ga_in->rt : 0;
   const GemvPlan p = gemv_plan(M, N, K, epi, force_waves, rt);
   if (p.waves == 0) return;  // callers check gemv_supported()
-  const bool xl = gemv_lds_bytes(p, M, K, true) <= kMaxLds;
-  int xm = xl ? kXLds : kXGlobal;
-  if (gemv_x_regs_for(epi) && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
   GemvArgs ga{};
   if (ga_in) ga = *ga_in;
   if (epi == MS_GEMV_EPI_ARGMAX || epi == MS_GEMV_EPI_ADD_F32 || epi == MS_GEMV_EPI_RESID_SSQ)
     ga.rs = RowScale{};  // argmax: r > 0 keeps every row's order; the others take unnormalised X
+  // the X image only when the block's whole LDS (image + factors + staged statistics) fits
+  const bool xl = gemv_lds_bytes(p, M, K, true, ga.rs) <= kMaxLds;
+  int xm = xl ? kXLds : kXGlobal;
+  if (gemv_x_regs_for(epi) && p.MT * p.U <= kXRegsMaxFrags) xm = kXRegs;
   if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = gemv_lds_bytes(p, M, K, xm == kXLds, ga.rs);
   if (lds > kMaxLds) return;

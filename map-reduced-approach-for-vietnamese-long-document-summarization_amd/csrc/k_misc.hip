@@ -37,10 +37,10 @@ __global__ __launch_bounds__(256) void embed_kernel(const int32_t* __restrict__ 
       const uint4 gv = *(const uint4*)(gamma + c * 8);
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
       uint4 o;
-      o.x = pack2h(a.x * h_lo(gw[0]), a.y * h_hi(gw[0]));
-      o.y = pack2h(a.z * h_lo(gw[1]), a.w * h_hi(gw[1]));
-      o.z = pack2h(b.x * h_lo(gw[2]), b.y * h_hi(gw[2]));
-      o.w = pack2h(b.z * h_lo(gw[3]), b.w * h_hi(gw[3]));
+      o.x = pack2h(a.x * h_lo(gw[0]) * kXgScale, a.y * h_hi(gw[0]) * kXgScale);
+      o.y = pack2h(a.z * h_lo(gw[1]) * kXgScale, a.w * h_hi(gw[1]) * kXgScale);
+      o.z = pack2h(b.x * h_lo(gw[2]) * kXgScale, b.y * h_hi(gw[2]) * kXgScale);
+      o.w = pack2h(b.z * h_lo(gw[3]) * kXgScale, b.w * h_hi(gw[3]) * kXgScale);
       *(uint4*)(xg + (size_t)t * H + c * 8) = o;
       ss += (a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w);
     }
@@ -153,10 +153,10 @@ __global__ __launch_bounds__(1024) void decode_tail_kernel(const float2* __restr
       const uint4 gv = *(const uint4*)(gamma + c * 8);
       const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w};
       uint4 o;
-      o.x = pack2h(a.x * h_lo(gw[0]), a.y * h_hi(gw[0]));
-      o.y = pack2h(a.z * h_lo(gw[1]), a.w * h_hi(gw[1]));
-      o.z = pack2h(bb.x * h_lo(gw[2]), bb.y * h_hi(gw[2]));
-      o.w = pack2h(bb.z * h_lo(gw[3]), bb.w * h_hi(gw[3]));
+      o.x = pack2h(a.x * h_lo(gw[0]) * kXgScale, a.y * h_hi(gw[0]) * kXgScale);
+      o.y = pack2h(a.z * h_lo(gw[1]) * kXgScale, a.w * h_hi(gw[1]) * kXgScale);
+      o.z = pack2h(bb.x * h_lo(gw[2]) * kXgScale, bb.y * h_hi(gw[2]) * kXgScale);
+      o.w = pack2h(bb.z * h_lo(gw[3]) * kXgScale, bb.w * h_hi(gw[3]) * kXgScale);
       *(uint4*)(xg + (size_t)b * H + c * 8) = o;
       ss += (a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w) + (bb.x * bb.x + bb.y * bb.y + bb.z * bb.z + bb.w * bb.w);
     }
@@ -212,8 +212,8 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const float* __restrict__ 
     float g0 = h_lo(wv.x), g1 = h_hi(wv.x);
     float g2 = h_lo(wv.y), g3 = h_hi(wv.y);
     uint2 o;
-    o.x = pack2h(v[k].x * g0, v[k].y * g1);
-    o.y = pack2h(v[k].z * g2, v[k].w * g3);
+    o.x = pack2h(v[k].x * g0 * kXgScale, v[k].y * g1 * kXgScale);
+    o.y = pack2h(v[k].z * g2 * kXgScale, v[k].w * g3 * kXgScale);
     *(uint2*)(yr + c * 4) = o;
   }
   ss = wave_sum(ss);
@@ -293,8 +293,8 @@ __global__ __launch_bounds__(256) void residual_rmsnorm_kernel(float* __restrict
     const float g0 = h_lo(wv[k].x), g1 = h_hi(wv[k].x);
     const float g2 = h_lo(wv[k].y), g3 = h_hi(wv[k].y);
     uint2 o;
-    o.x = pack2h(v[k].x * g0, v[k].y * g1);
-    o.y = pack2h(v[k].z * g2, v[k].w * g3);
+    o.x = pack2h(v[k].x * g0 * kXgScale, v[k].y * g1 * kXgScale);
+    o.y = pack2h(v[k].z * g2 * kXgScale, v[k].w * g3 * kXgScale);
     *(uint2*)(yr + c * 4) = o;
   }
   ss = wave_sum(ss);

@@ -625,8 +625,13 @@ static QPlan qplan(int M, int N, int K, int epi, int rt = 0) {  // K: per-split 
 
 static constexpr size_t kLdsCap = 160 * 1024;
 
-static bool qx_in_lds(int M, int K) {
-  return gemv_x_lds_bytes(M, K) <= kLdsCap;
+// the X image is staged in LDS only when the whole block's LDS -- the image, the deferred-norm
+// factors and the staged statistics (gemv_lds_total) -- fits; a shape whose image alone fits
+// (M = 40 at K = 2048: exactly 160 KiB) takes the global-X path instead of being refused
+// (a refused split once made one row group of a K-quant batch fall back to an unsplit slab
+// while the others split 4 ways, and the residual fold then dropped slabs of every row)
+static bool qx_in_lds(int M, int K, const RowScale& rs = RowScale{}) {
+  return gemv_lds_total(gemv_x_lds_bytes(M, K), rs, M) <= kLdsCap;
 }
 
 static bool qx_in_regs(const QPlan& p) {
@@ -635,14 +640,14 @@ static bool qx_in_regs(const QPlan& p) {
   return want && p.MT * p.SBW == 1;
 }
 
-static size_t qlds_main(const QPlan& p, int M, int K) {
+static size_t qlds_main(const QPlan& p, int M, int K, const RowScale& rs = RowScale{}) {
   // X image (when it fits and X is not taken into registers)
-  const size_t xs = (!qx_in_regs(p) && qx_in_lds(M, K)) ? gemv_x_lds_bytes(M, K) : 0;
+  const size_t xs = (!qx_in_regs(p) && qx_in_lds(M, K, rs)) ? gemv_x_lds_bytes(M, K) : 0;
   const size_t red = (size_t)p.waves * p.MT * p.NT * 256 * 4;
   return xs > red ? xs : red;
 }
 static size_t qlds(const QPlan& p, int M, int K, const RowScale& rs = RowScale{}) {
-  return gemv_lds_total(qlds_main(p, M, K), rs, M);
+  return gemv_lds_total(qlds_main(p, M, K, rs), rs, M);
 }
 
 bool qgemv_supported(int M, int N, int K, int epi, int rs_tiles) {
@@ -666,12 +671,12 @@ static void qgemv_go(const f16_t* X, const QMat& q, void* out, int M, int N, int
   if (EPI == MS_GEMV_EPI_ARGMAX || EPI == MS_GEMV_EPI_ADD_F32) ga.rs = RowScale{};  // r > 0 keeps the order
   if (ga.rs.ssq && rs_stage_floats(ga.rs, M) == 0) return;  // callers check gemv_rs_supported
   const size_t lds = qlds(p, M, K, ga.rs);
-  const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K));
+  const int ro = (int)gemv_rinv_offset(qlds_main(p, M, K, ga.rs));
   const dim3 grid(p.tiles, S), blk(64 * p.waves);
   if constexpr ((EPI == MS_GEMV_EPI_ROPE_KV || EPI == MS_GEMV_EPI_RESID_SSQ) && MT != 1) {
     return;
   } else {
-    const bool xl = qx_in_lds(M, K);
+    const bool xl = qx_in_lds(M, K, ga.rs);
     constexpr bool kRsEpi = gemv_rs_epi<EPI>();
     const bool rs = kRsEpi && ga.rs.ssq != nullptr;
 #define QL(SBW_, XM_)                                                                                         \

@@ -56,10 +56,21 @@ struct RowScale {
 inline RowScale make_row_scale(const float* ssq, int tiles, int H, float eps) {
   return RowScale{ssq, tiles, H, eps, 1.0f / (float)H};
 }
-// rinv = rsq(sum / H + eps): one v_rsq_f32 (1 ulp) -- the same instruction sequence in every
-// consumer, so every kernel derives the identical factor from the identical sum
+// The producers store the GEMM input pre-scaled by an exact power of two, xg = f16(x * g * 2^-4),
+// and every consumer folds 2^4 into the row factor: r' = 16 rsq(...).  Both scalings are exact
+// in fp32, and f16(v * 2^-4) = f16(v) * 2^-4 wherever v is a normal fp16 value, so the products
+// r' * (xg . W) are bit-identical to r * (f16(x * g) . W) there -- but the un-normalised residual
+// (massive activations of real checkpoints reach 1e3-1e4 in a few channels; x * g is NOT
+// normalised before the rounding) now overflows fp16 only beyond |x * g| = 16 * 65504 ~ 1e6
+// instead of 65504.  Below |x * g| = 2^-10 the value lands in fp16's subnormals,
+// whose absolute step 2^-20 is the normal step at that magnitude: no precision is lost where
+// it matters for a dot product.
+constexpr float kXgScale = 0.0625f, kXgUnscale = 16.0f;
+// rinv = 16 rsq(sum / H + eps): one v_rsq_f32 (1 ulp) and an exact power-of-two multiply -- the
+// same instruction sequence in every consumer, so every kernel derives the identical factor
+// from the identical sum
 __device__ __forceinline__ float rs_rinv(float sum, const RowScale& rs) {
-  return __builtin_amdgcn_rsqf(__fmaf_rn(sum, rs.inv_h, rs.eps));
+  return __builtin_amdgcn_rsqf(__fmaf_rn(sum, rs.inv_h, rs.eps)) * kXgUnscale;
 }
 
 // x = the embedding rows; with gamma also xg = f16(x * gamma) and ssq = per-row sums of x^2

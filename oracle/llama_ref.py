@@ -166,6 +166,8 @@ class OracleLlama:
             """(GEMM input, per-row factor applied after the GEMM)."""
             if f16:  # ggml: rms_norm then mul by g in fp32, the matmul rounds its input
                 return _f16((x * rms_rinv_f64(x, eps)) * g), np.float32(1.0)
+            if self.mode == "engine":  # kernels.h kXgScale: f16(x g 2^-4), 16 r -- exact scalings
+                return rnd((x * g).astype(np.float32) * np.float32(0.0625)), rms_rinv(x, eps) * np.float32(16.0)
             return norm_input(x, g, rnd), rms_rinv(x, eps)
 
         pre = _f32 if f16 else rnd  # Q/K/V before RoPE: ggml keeps them fp32

@@ -19,6 +19,9 @@ from oracle.llama_ref import OracleLlama  # noqa: E402
 from oracle.synth import make_weights  # noqa: E402
 
 SEED = 1234
+# kernels.h kXgScale / kXgUnscale: the deferred-norm GEMM input is stored as f16(x * g * 2^-4) and
+# every consumer's row factor carries the 2^4 back (exact power-of-two scalings)
+XG_SCALE, XG_UNSCALE = 0.0625, 16.0
 STD = 0.05  # large enough that attention/MLP, not the tied embedding, drive the tokens
 JITTER = 0.1
 
@@ -233,7 +236,7 @@ def test_residual_rmsnorm(lib, dev, S):
                                        ssq.data_ptr(), rows, H, _stream()))
     torch.cuda.synchronize()
     assert torch.equal(x, xr) if S else torch.equal(x, x0)  # same adds in the same order
-    assert torch.equal(y, (xr * w.float()).to(torch.float16))  # one RNE rounding of x * w
+    assert torch.equal(y, (xr * w.float() * XG_SCALE).to(torch.float16))  # one RNE rounding of x * w * 2^-4
     assert rel(ssq.double().cpu(), _ssq_ref(xr.cpu())) < 1e-6
     y2 = torch.empty_like(y)
     ssq2 = torch.empty_like(ssq)
@@ -263,7 +266,7 @@ def test_gemv_resid_epilogue(lib, dev, M, rt):
                                  ssq.data_ptr(), M, N, K, rt, _stream()))
     torch.cuda.synchronize()
     assert rel(x.double().cpu(), x_ref) < 1e-6
-    want = (x * gamma.float()).to(torch.float16)  # from the stored x exactly
+    want = (x * gamma.float() * XG_SCALE).to(torch.float16)  # from the stored x exactly
     bad = (xg != want).nonzero()
     if bad.numel():
         i, j = bad[0].tolist()
@@ -285,7 +288,7 @@ def test_gemv_resid_epilogue(lib, dev, M, rt):
         L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
     torch.cuda.synchronize()
     xd = x.double().cpu()
-    r = 1.0 / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
+    r = XG_UNSCALE / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
     exp = r * (xg.double().cpu() @ Wq.double().cpu().T)
     assert rel(out.double().cpu(), exp) < 1e-5
 
@@ -312,7 +315,7 @@ def test_gemm_resid_epilogue(lib, dev, M, variant):
                                      ssq.data_ptr(), M, N, K, _stream()))
         torch.cuda.synchronize()
         assert rel(x.double().cpu(), x_ref) < 1e-6
-        want = (x * gamma.float()).to(torch.float16)
+        want = (x * gamma.float() * XG_SCALE).to(torch.float16)
         assert int((xg != want).sum()) == 0
         tw = N // tiles
         for t in (0, tiles // 2, tiles - 1):
@@ -331,7 +334,7 @@ def test_gemm_resid_epilogue(lib, dev, M, variant):
     finally:
         L.check(lib.ms_set_gemm_variant(0))
     xd = x.double().cpu()
-    r = 1.0 / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
+    r = XG_UNSCALE / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
     exp = r * (xg.double().cpu() @ Wq.double().cpu().T)
     assert rel(out.double().cpu(), exp) < 1e-5
 
@@ -345,7 +348,7 @@ def test_row_scale_epilogues(lib, dev, path):
     M, K, eps = 8, 3072, 1e-5
     X = _f16(torch.randn(M, K, generator=g)).to(dev)
     ssq = (torch.rand(M, generator=g) * 5000 + 100).to(dev)
-    r = (1.0 / torch.sqrt(ssq.double().cpu() / K + eps))[:, None]
+    r = (XG_UNSCALE / torch.sqrt(ssq.double().cpu() / K + eps))[:, None]
     ws = torch.zeros(256, dtype=torch.uint8, device=dev)
     L.check(lib.ms_op_set_row_scale(ssq.data_ptr(), 1, K, eps))
     try:
@@ -474,7 +477,7 @@ def test_rmsnorm_and_argmax(lib, dev):
                               _stream()))
     torch.cuda.synchronize()
     xs = x.flip(0)
-    assert torch.equal(y, (xs * w.float()).to(torch.float16))
+    assert torch.equal(y, (xs * w.float() * XG_SCALE).to(torch.float16))
     assert rel(ssq.double().cpu(), _ssq_ref(xs.cpu())) < 1e-6
     lg = torch.randn(5, 128256, generator=g).to(dev)
     lg[2, 77] = 100.0
@@ -941,12 +944,14 @@ def test_q4_gate_up_grid_stride_bit_exact(lib, dev, M, N, K, rs):
 
 
 @pytest.mark.parametrize("qtype", [Q.GGML_TYPE_Q4_K, Q.GGML_TYPE_Q6_K])
-@pytest.mark.parametrize("M", [1, 8, 16])
+@pytest.mark.parametrize("M", [1, 8, 16, 33, 40, 64])
 @pytest.mark.parametrize("N,K,S", [(256, 3072, 6), (512, 3072, 4), (128, 8192, 4), (256, 8192, 2),
                                    (64, 768, 3)])
 def test_qgemv_split_slabs_vs_fp64(lib, dev, qtype, M, N, K, S):
     """Quantised split-K: slab s is the dequantised partial product over its K range (fp32
-    sum order only); the slabs add up to the full product; bad splits are refused."""
+    sum order only); the slabs add up to the full product; bad splits are refused.  Every
+    row-group size of a K-quant batch is supported (M = 40 at K / S = 2048: an X image of
+    exactly 160 KiB takes the global-X path -- the round-5 row-group bug)."""
     b, wbf, pk = _packed(lib, dev, qtype, N, K, 11 + M + S)
     g = torch.Generator(device="cpu").manual_seed(M + N + K + S)
     X = torch.randn(M, K, generator=g).to(torch.float16).to(dev)
@@ -1084,3 +1089,37 @@ def test_wide_hidden_prefill_takes_the_plain_residual_path(dev):
         assert err < 2e-2
         got = e.generate([ids], num_predict=6, ignore_eos=True)[0].ids
         assert len(got) == 6
+
+
+def test_large_residual_rows_stay_finite(dev):
+    """The deferred RMSNorm feeds the projections f16(x * g) of the UN-normalised residual, so a
+    real checkpoint's massive activations (1e3-1e4 in a few channels) times a large gain could
+    pass fp16's 65504 where ggml, which normalises first, would not.  The producers
+    pre-scale by 2^-4 (kernels.h kXgScale, exact): here every norm gain is 4 and the embedding
+    sits near fp16's maximum, so |x * g| reaches ~2.5e5 -- inf without the pre-scale -- and the
+    engine must still match un-rounded fp32 Llama within 2e-2 and decode without a failed row."""
+    from oracle.synth import f16_rne
+    w = make_weights(TINY, SEED, std=STD, jitter=0.0)
+    emb = f16_rne(np.clip(w["embed"] * 6.0e5, -60000.0, 60000.0))
+    w["embed"] = w["lm_head"] = emb
+    gain = np.full(TINY.hidden, 4.0, np.float32)
+    w["final_norm"] = gain
+    for ly in w["layers"]:
+        ly["attn_norm"] = gain
+        ly["ffn_norm"] = gain
+    assert float(np.max(np.abs(emb)) * 4.0) > 65504.0 * 2  # the old fp16 input would overflow
+    oracle = OracleLlama(TINY, w, mode="fp32")
+    ids = np.random.default_rng(29).integers(0, 4000, size=160).astype(np.int32)
+    with Engine(TINY, device=0, max_batch=2, max_ctx=512, max_prefill_tokens=1024) as e:
+        load_logical(e, w)
+        _, lg = e.forward(ids, hidden=False, logits=True)
+        res = e.generate([ids], num_predict=8, ignore_eos=True)[0]
+    assert np.all(np.isfinite(lg))
+    ref, _ = oracle.forward(ids, all_logits=True)
+    err = rel(lg, ref)
+    print(f"|x * g| up to {float(np.max(np.abs(emb))) * 4:.3g}: prefill logits rel err {err:.3e}, ids {res.ids}")
+    assert err < 2e-2
+    assert res.finish == "length" and len(res.ids) == 8
+    a, flips = _teacher_forced_agreement(oracle, ids, res.ids)
+    for pos, gap, top in flips:
+        assert gap <= 1e-2 * (abs(top) + 1.0), (pos, gap, top)
