@@ -51,14 +51,29 @@ def synthetic_chunks(n, prompt_len, doc, vocab, bos, seed=0, first_chunk=0):
     return out
 
 
-def gemv_bytes_per_step(cfg, B):
+def gemv_bytes_per_step(cfg, B, qkv_fused=False):
     """Algorithmic HBM bytes of one decode step's layer projections: every weight matrix
-    once + the B activation rows in/out (SURVEY.md §8d weight term, without lm_head)."""
+    once + the B activation rows in/out (SURVEY.md §8d weight term, without lm_head).
+    qkv_fused: the QKV projection runs inside the fused QKV + attention launch (k_qkvattn.hip),
+    so the GEMV launches stream O / gate-up / down only."""
     H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
     qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
     w = 2 * (qkv * H + H * cfg.n_heads * D + 2 * F * H + H * F)
     act = 2 * B * (H + qkv + cfg.n_heads * D + H + H + F + F + H) + 4 * B * H * 4
+    if qkv_fused:
+        w -= 2 * qkv * H
+        act -= 2 * B * (H + qkv)
     return cfg.n_layers * (w + act)
+
+
+def qkv_attn_bytes_per_launch(cfg, B, kv_keys):
+    """The fused QKV + attention launch of one layer: the QKV weights, its B input rows, the
+    fp32 projection handed off (written once, read once), and the K/V of kv_keys cached keys
+    summed over the batch (SURVEY.md §8d's KV-read term) plus the new tokens' K/V."""
+    H, D = cfg.hidden, cfg.head_dim
+    qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
+    kv_tok = 2 * cfg.n_kv_heads * D * 2
+    return 2 * qkv * H + 2 * B * H + 2 * 4 * B * qkv + kv_keys * kv_tok + B * kv_tok
 
 
 def _q4_k_m_bytes_per_weight(tensor, layer, n_layers):
@@ -126,8 +141,11 @@ def cpu_baseline(cfg, prompt_ids, gen_len, decode_sample=64):
     torch.set_num_threads(threads)
     phys = _physical_cores()
     r = time_chunk(cfg, prompt_ids, gen_len, decode_sample=decode_sample)
+    # numerics: bf16, not the engine's fp16 -- torch's CPU GEMM has no fp16 fast path (measured in
+    # the build container: 266 GF/s fp16 vs 1252 GF/s bf16 at 256 x 8192 x 3072, 8 threads), so an
+    # fp16 sample would time torch's fp16 emulation, not a CPU running this model
     return {"value": round(1.0 / r["chunk_s"], 5), "unit": "chunks/s", "cores": int(r["threads"]),
-            "kind": "port", "cpu_model": r["cpu_model"],
+            "kind": "port", "dtype": "bf16", "cpu_model": r["cpu_model"],
             "sample": (f"CPU restatement (not Ollama): torch {torch.__version__} CPU bf16 on {r['cpu_model']}, "
                        f"{r['threads']} threads = every CPU this process may use (affinity mask {allowed}, "
                        f"cgroup quota {quota if quota else 'none'}; {phys} physical cores on the host), "
@@ -324,22 +342,23 @@ def main():
                  "batch_invariant_chunk0": alone == outs[0][0]}
         assert same and full and check["batch_invariant_chunk0"], check
 
-    roof = None
+    roof = roof_qa = None
     if not args.no_roofline:
         # Roofline of the dominant kernel class (the decode weight stream): one more map
         # step with HIP events bracketing every GEMV launch on the engine's stream.  It
         # runs after the timed region because an event pair per launch (113 per decode
         # step) costs ~0.6 ms/step and would distort `value`.
         eng.reset_stats()
-        eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD))
+        eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD) | (1 << L.K_QKV_ATTN))
         eng.generate(chunks[:min(len(chunks), B)], num_predict=min(args.gen_len, 64), ignore_eos=True)
         eng.set_profiling(0)
         sp = eng.stats()
         launches = sp["kernel_launches"][L.K_GEMV] + sp["kernel_launches"][L.K_LMHEAD]
+        n_qa = sp["kernel_launches"][L.K_QKV_ATTN]
         if launches:
             gemv_s = (sp["kernel_ms"][L.K_GEMV] + sp["kernel_ms"][L.K_LMHEAD]) / 1e3
             bstep = sp["decode_tokens"] / max(sp["decode_steps"], 1)
-            per_step = (qgemv_bytes_per_step(cfg, bstep) if quant else gemv_bytes_per_step(cfg, bstep)) \
+            per_step = (qgemv_bytes_per_step(cfg, bstep) if quant else gemv_bytes_per_step(cfg, bstep, n_qa > 0)) \
                 + lm_head_bytes_per_step(cfg, bstep, quant)
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
@@ -351,6 +370,20 @@ def main():
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
                     "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}
+            if n_qa:
+                # the fused QKV + attention launch (k_qkvattn.hip) streams the QKV weights and the
+                # K/V together: its own HBM roofline entry; the GEMV class above excludes QKV
+                roof["kernel"] = "gemv_kernel (fp16 decode weight stream: O/gate-up/down projections + lm_head)"
+                qa_s = sp["kernel_ms"][L.K_QKV_ATTN] / 1e3
+                qa_bytes = (qkv_attn_bytes_per_launch(cfg, bstep, 0) * n_qa
+                            + sp["decode_kv_tokens"] * cfg.n_layers * 2 * cfg.n_kv_heads * cfg.head_dim * 2)
+                qa_gbs = qa_bytes / qa_s / 1e9
+                roof_qa = {"bound": "hbm", "achieved": round(qa_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(qa_gbs / HBM_PEAK_GBS, 4), "kernel": "qkv_attn_kernel (fused QKV "
+                           "projection + decode attention, one launch per layer)",
+                           "bytes_per_launch": int(qa_bytes / n_qa), "avg_launch_us": round(qa_s / n_qa * 1e6, 2),
+                           "method": "QKV weights + fp32 hand-off + K/V read (decode_kv_tokens) per event-timed "
+                                     "launch, the same extra untimed map step"}
     # whole-phase rooflines from the timed run's own event-timed prefill / decode passes
     pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * n_local * args.steps
     pre_tf = pre_flops / (st["prefill_ms"] / 1e3) / 1e12 if st["prefill_ms"] else None
@@ -400,6 +433,7 @@ def main():
         "roofline": roof,
         "roofline_prefill": roof_pre,
         "roofline_decode": roof_dec,
+        "roofline_qkv_attn": roof_qa,
         "check": check,
         "cpu_baseline": None,
     }

@@ -116,7 +116,9 @@ typedef struct ms_stats {
   double prefill_ms, decode_ms; /* device time (events) when profiling is on   */
   double kernel_ms[8];          /* per kernel class, when profiling is on:
                                    0 gemm(prefill) 1 attn_prefill 2 gemv(decode)
-                                   3 attn_decode 4 lm_head 5 norm/rope/misc     */
+                                   3 attn_decode 4 lm_head 5 norm/rope/misc
+                                   6 qkv_attn (the fused QKV projection + decode
+                                   attention of <= 8-slot engines)              */
   int64_t kernel_launches[8];
   int64_t decode_kv_tokens;     /* sum over decode steps and rows of the keys attended
                                    (the KV-read term of SURVEY.md §8d's decode bytes)  */
@@ -185,6 +187,9 @@ int ms_set_profiling(ms_engine* e, uint32_t class_mask);
 int ms_trace_push(const char* name);
 int ms_trace_pop(void);
 int ms_synchronize(ms_engine* e);
+/* diagnostic: the fused QKV + attention launch's phase stamps of its latest launch, [256][16]
+   s_memrealtime ticks (100 MHz), recorded only under MS_QA_STAMPS=1 (tools/qa_stamps.py) */
+int ms_debug_qa_stamps(uint64_t* out, int32_t n);
 
 /* ---- parity probe (tests): one prompt through the prefill path -------------- */
 /* hidden_out: [n][hidden] fp32 residual after `n_layers_run` layers (or NULL);

@@ -68,7 +68,7 @@ struct MsError : std::runtime_error {
     if (!(cond)) throw MsError((code), (msg));        \
   } while (0)
 
-enum KClass { K_GEMM = 0, K_ATTN_PREFILL = 1, K_GEMV = 2, K_ATTN_DECODE = 3, K_LMHEAD = 4, K_MISC = 5 };
+enum KClass { K_GEMM = 0, K_ATTN_PREFILL = 1, K_GEMV = 2, K_ATTN_DECODE = 3, K_LMHEAD = 4, K_MISC = 5, K_QKV_ATTN = 6 };
 
 struct Seq {
   uint64_t tag = 0;
@@ -151,6 +151,21 @@ struct ms_engine {
   unsigned* attn_cnt = nullptr;  // [max_batch * Hk] arrival counters, zero between launches
   bool attn2_ok(int B, int max_len) const {
     return attn_v2 && slot_major && attn_decode2_supported(B, Hq, Hk, max_len, attn_ppb);
+  }
+  // the QKV projection and decode attention as one launch (k_qkvattn.hip, MS_QKV_ATTN=1): engines
+  // of <= 8 slots on fp16 QKV weights with the v2 attention plan; chosen per engine at creation
+  // (qkv_attn_supported at max_batch / max_ctx holds for every step) and bit-identical to the
+  // split-6 GEMV + v2 attention it replaces.  Opt-in: measured SLOWER, 32.4-35.4 vs 8.2 + 18.4 us
+  // per layer (decode 2.25-2.33 vs 2.09 ms per step, profiles/r05/v6_*): a CU's memory
+  // operations retire in order across its waves, so the hand-off (publish drain, arrival, poll,
+  // prologue reads) either queues behind the K/V pages in flight on its CU or the pages wait for
+  // the hand-off -- in-kernel stamps put publish -> poll at 6-7 us, against ~1.5 us for a kernel
+  // boundary.  qa_used: a launch since the last error check (shares the hand-off timeout flag
+  // mlp_sync_d[16]; its counters are mlp_sync_d[32..48])
+  bool qkv_attn = false, qa_used = false;
+  bool qkv_attn_on(const QSlot* q, int B, int max_len) const {
+    return qkv_attn && attn_slabs && !(q && q->ready()) && attn2_ok(B, max_len) &&
+           qkv_attn_supported(B, cfg.max_batch, H, Hq, Hk, max_len, attn_ppb, split_qkv);
   }
   void attn_decode(const DecodeQKV& qa, const KVView& kv, const DecodeAttnArgs& da) {
     prof_begin(K_ATTN_DECODE);
@@ -490,7 +505,16 @@ struct ms_engine {
     const auto& Q = lq[l];
     const RowScale rs_attn = cur_rs;
     DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab, rs_attn};
-    if (attn_slabs) {
+    const bool fused_qa = qkv_attn_on(&Q[QS_QKV], B, da.max_len);
+    if (fused_qa) {
+      // one launch: the QKV rows (slab 0 holds the folded split-6 sums) and attention
+      qa.S = 1;
+      prof_begin(K_QKV_ATTN);
+      launch_qkv_attn(xb, Ly.wqkv, slabs, qa, attn, Hq, Hk, kv, da, attn_ws, attn_ppb, mlp_sync_d + 32,
+                      mlp_sync_d + 16, stream);
+      prof_end(K_QKV_ATTN);
+      qa_used = true;
+    } else if (attn_slabs) {
       // QKV -> unscaled slabs; attention adds them, applies the row's deferred-norm factor and
       // RoPE, and writes the new K/V (k_attn.hip): one factor per attention block, not per
       // QKV tile
@@ -509,7 +533,7 @@ struct ms_engine {
       proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
       qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}};
     }
-    attn_decode(qa, kv, da);
+    if (!fused_qa) attn_decode(qa, kv, da);
     resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm);
     const RowScale rs_ffn = cur_rs;
     const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
@@ -846,6 +870,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_MLP_FUSED")) E.mlp_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_DECODE_TAIL")) E.tail_fuse = atoi(v) != 0;
+    if (const char* v = getenv("MS_QKV_ATTN")) E.qkv_attn = atoi(v) != 0;
     if (const char* v = getenv("MS_QRESID")) E.qresid = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
@@ -1506,22 +1531,24 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
   HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_ring_d, (size_t)k * B * sizeof(int32_t), hipMemcpyDeviceToHost,
                         E.stream));
-  if (E.mlp_used)
+  if (E.mlp_used || E.qa_used)
     HIP_OK(hipMemcpyAsync(E.mlp_err_h, E.mlp_sync_d + 16, sizeof(unsigned), hipMemcpyDeviceToHost, E.stream));
   ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
-  if (E.mlp_used && *E.mlp_err_h) {  // a workgroup of the fused MLP was not resident: never silent
+  if ((E.mlp_used || E.qa_used) && *E.mlp_err_h) {  // a workgroup of a fused launch was not resident: never silent
     // fall back to the two launches for good: clear the device flag and the counters, and drop
     // every captured graph that still holds mlp_decode_kernel; the run's ids are discarded (the
     // sequences did not advance), so the next ms_step recomputes them unfused
     E.mlp_fuse = false;
     E.mlp_used = false;
+    E.qkv_attn = false;
+    E.qa_used = false;
     HIP_OK(hipMemsetAsync(E.mlp_sync_d, 0, 64 * sizeof(unsigned), E.stream));
     HIP_OK(hipStreamSynchronize(E.stream));
     *E.mlp_err_h = 0;
     E.drop_graphs();
-    REQUIRE(false, MS_EIO, "fused decode MLP: hand-off timed out (not every workgroup resident); "
-                           "fusion disabled for this engine, the run's ids were discarded");
+    REQUIRE(false, MS_EIO, "fused decode launch (MLP / QKV + attention): hand-off timed out (not every "
+                           "workgroup resident); fusion disabled for this engine, the run's ids were discarded");
   }
   std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));
 }
@@ -1684,6 +1711,12 @@ int ms_reset_stats(ms_engine* e) {
 int ms_set_profiling(ms_engine* e, uint32_t mask) {
   if (!e) return MS_EINVAL;
   e->prof_mask = mask;
+  return MS_OK;
+}
+
+int ms_debug_qa_stamps(uint64_t* out, int32_t n) {
+  if (!out || n < 0) return MS_EINVAL;
+  ms::qkv_attn_stamps(reinterpret_cast<unsigned long long*>(out), n);
   return MS_OK;
 }
 

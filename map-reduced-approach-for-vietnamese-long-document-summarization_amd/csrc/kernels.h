@@ -274,6 +274,22 @@ size_t attn_decode2_workspace_bytes(int B, int Hq, int max_len, int ppb);
 void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv, DecodeAttnArgs a,
                          float* ws, int ppb, hipStream_t s, unsigned* cnt = nullptr);
 
+// merge nsplit decode-attention partials (launch_attn_decode2's workspace layout) into out
+void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int nsplit, hipStream_t s);
+
+// The decode step's QKV projection and attention as ONE launch (k_qkvattn.hip): 256 workgroups
+// (one per CU, all resident) each compute 20 rows of the QKV projection -- bit-identical to the
+// split-6 GEMV + slab fold -- publish them (write-through) to qkv32 [B][QKVN] behind a per-kv-head
+// arrival counter, and run one (sequence, kv head, split) item of launch_attn_decode2 (ppb page
+// waves) whose K/V pages are already in flight.  sync: >= 32 zeroed words the kernel leaves zeroed;
+// err: set when a hand-off wait gives up (a workgroup was not resident) -- never a hang.
+bool qkv_attn_supported(int B, int max_batch, int H, int Hq, int Hk, int max_len, int ppb, int split_qkv);
+// diagnostic: the latest launch's phase stamps [256][16] (MS_QA_STAMPS=1), 100 MHz ticks
+void qkv_attn_stamps(unsigned long long* host, int n);
+void launch_qkv_attn(const f16_t* xb, const f16_t* wqkv, float* qkv32, const DecodeQKV& qa, f16_t* out, int Hq,
+                     int Hk, KVView kv, DecodeAttnArgs a, float* ws, int ppb, unsigned* sync, unsigned* err,
+                     hipStream_t s);
+
 // synthetic weights (oracle/synth.py restates this generator)
 // row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the
 // rope permutation dst_row = (r & ~127) + rope_perm(r & 127) + map_add

@@ -23,7 +23,7 @@ MS_EPI_STORE_F16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
 MS_EPI_ARGMAX = 5
 MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms
-K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC = range(6)
+K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC, K_QKV_ATTN = range(7)
 
 EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
@@ -35,7 +35,7 @@ EXPORTED = (
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
     "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
-    "ms_trace_push", "ms_trace_pop",
+    "ms_trace_push", "ms_trace_pop", "ms_debug_qa_stamps",
 )
 
 
@@ -125,6 +125,7 @@ def load() -> C.CDLL:
         "ms_declare_weight_q": (i32, [vp, i32, i32, i32]),
         "ms_trace_push": (i32, [C.c_char_p]),
         "ms_trace_pop": (i32, []),
+        "ms_debug_qa_stamps": (i32, [vp, i32]),
     }
     ab = bool(os.environ.get("MAPSUM_LIB"))  # an A/B build may predate the newest op hooks
     for name, (res, args) in sig.items():

@@ -480,6 +480,64 @@ def test_fused_decode_mlp_timeout_recovers(dev, chunks, monkeypatch):
         e.close()
 
 
+def _qa_run(prompts, gen, monkeypatch, fused, slots=NCHUNK, ctx=P + 64):
+    monkeypatch.setenv("MS_QKV_ATTN", fused)
+    e = Engine(CFG, device=0, max_batch=slots, max_ctx=ctx, max_prefill_tokens=NCHUNK * P)
+    try:
+        e.init_synthetic(SEED, STD, JIT)
+        e.set_profiling(1 << L.K_QKV_ATTN)
+        res = e.generate(list(prompts), num_predict=gen, ignore_eos=True)
+        e.set_profiling(0)
+        return [r.ids for r in res], e.stats()["kernel_launches"][L.K_QKV_ATTN]
+    finally:
+        e.close()
+
+
+def test_fused_qkv_attention_bit_exact(dev, chunks, monkeypatch):
+    """The decode step's QKV projection and attention as one launch (k_qkvattn.hip, opt-in: 20 QKV
+    rows per workgroup, a per-kv-head hand-off, the K/V pages in flight after the publish) against
+    the split-6 GEMV + v2 attention launches it replaces: identical greedy ids on the bench
+    workload (8 x 2048-token chunks, 8 slots), and the fused kernel really ran (one launch per
+    layer per decode step)."""
+    got, n_fused = _qa_run(chunks, 48, monkeypatch, "1")
+    want, n_plain = _qa_run(chunks, 48, monkeypatch, "0")
+    assert n_plain == 0 and n_fused >= CFG.n_layers * 40, (n_fused, n_plain)
+    assert got == want
+
+
+def test_fused_qkv_attention_ragged_bit_exact(dev, chunks, monkeypatch):
+    """Ragged prompts (1 .. 33 pages: splits without pages, a new token on a page boundary,
+    fewer sequences than slots, so fewer attention items than workgroups) through the fused
+    launch and the two launches: identical ids."""
+    prompts = [chunks[i][:n] for i, n in enumerate((5, 63, 64, 65, 700, 1500, 2047))]
+    got, n_fused = _qa_run(prompts, 40, monkeypatch, "1")
+    want, _ = _qa_run(prompts, 40, monkeypatch, "0")
+    assert n_fused > 0
+    assert got == want
+
+
+def test_fused_qkv_attention_timeout_recovers(dev, chunks, monkeypatch):
+    """A hand-off timeout of the fused QKV + attention launch (forced: MS_QA_SPIN=0) fails the
+    step with MS_EIO and leaves the engine usable on the two-launch path, with its exact ids."""
+    want, _ = _qa_run(chunks[:2], 24, monkeypatch, "0")
+    monkeypatch.setenv("MS_QKV_ATTN", "1")
+    monkeypatch.setenv("MS_QA_SPIN", "0")
+    e = Engine(CFG, device=0, max_batch=NCHUNK, max_ctx=P + 64, max_prefill_tokens=NCHUNK * P)
+    try:
+        e.init_synthetic(SEED, STD, JIT)
+        tags = [e.submit(c, 24, ignore_eos=True) for c in chunks[:2]]
+        with pytest.raises(RuntimeError, match="hand-off timed out"):
+            e.step()
+        for _ in range(64):
+            if e.step() == 0:
+                break
+        e.collect()
+        got = e.take(tags)
+        assert [got[t].ids for t in tags] == want
+    finally:
+        e.close()
+
+
 @pytest.mark.parametrize("slots", [NCHUNK, 32])
 def test_decode_tail_bit_exact(dev, chunks, monkeypatch, slots):
     """The one-launch decode step tail (k_misc.hip decode_tail_kernel: the lm_head partials'
