@@ -228,7 +228,8 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
 int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const void* gamma, float* ssq_out,
                      int32_t M, int32_t N, int32_t K, void* stream);
 int ms_gemm_resid_tiles(int32_t M, int32_t N);
-/* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase) */
+/* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase,
+   3 = 256x256 on 4 waves; bit-identical to 2) */
 int ms_set_gemm_variant(int32_t variant);
 /* tuning/test hook: the K-quant GEMVs that have a grid-stride two-stage form (the Q6_K lm_head
    argmax, the Q4_K gate/up SwiGLU) take it (1, the default) or run one-tile blocks (0); the

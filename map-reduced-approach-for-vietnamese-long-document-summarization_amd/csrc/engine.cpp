@@ -1844,7 +1844,7 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
 int ms_gemm_resid_tiles(int32_t M, int32_t N) { return gemm_resid_tiles(M, N); }
 
 int ms_set_gemm_variant(int32_t v) {
-  if (v < 0 || v > 2) return MS_EINVAL;
+  if (v < 0 || v > 3) return MS_EINVAL;
   set_gemm_variant(v);
   return MS_OK;
 }

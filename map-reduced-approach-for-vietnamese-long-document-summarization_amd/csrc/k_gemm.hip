@@ -531,12 +531,237 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   }
 }
 
+// ---- 4-wave 256x256x64 variant (gemm variant 3, opt-in): 256 threads in 2 x 2, each wave a 128 x 128
+// output (8 x 8 MFMA tiles, the 256 accumulators pinned in AGPRs, one wave per SIMD) -- the library
+// GEMM's geometry at this shape (hipBLASLt MT256x256x64_MI16x16 on 4 waves: 1455 vs 1215 TF/s on
+// the gate/up shape, same box, profiles/r05/v8_*).  Per K-tile a wave reads 32 KB of fragments for
+// 128 MFMAs (the 8-wave kernel: 24 KB for 64).  One barrier per K-tile, every LDS read and DMA
+// instruction slotted between MFMAs (one per two, the library kernel's interleave): the MFMAs of
+// k-step 0 carry the fragment reads of k-step 1; then vmcnt(0) + barrier (tile t+1 has landed
+// everywhere, tile t is no longer read); the MFMAs of k-step 1 carry tile t+2's DMA into tile t's
+// buffer and tile t+1's k-step-0 reads.  Same LDS image and swizzle as gemm256_kernel, same k order
+// per output element (x as the initial accumulator of the residual epilogue, 32-k MFMAs in k
+// order), same statistics order: every result is bit-identical to gemm256_kernel's
+// (test_gemm_4wave_bit_exact).  Measured (profiles/r05/v9_*, v10_*): 1002-1415 TF/s against the
+// 8-wave kernel's 1016-1327 -- ahead on square shapes, level on the prefill ones; a 4-slot ring of
+// 32-k steps (three steps of DMA lookahead, 64-B row segments) was slower (1029-1259).  Not the
+// default: the library kernel's remaining 15-25 % is not in this schedule.
+template <int EPI>
+__global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict__ A,
+                                                       const f16_t* __restrict__ W,
+                                                       void* __restrict__ out, int M, int N, int K,
+                                                       int ldo, RowScale rs, GemmResid gr) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * 65536 + TBM * 4 * (1 + kGemmRsTiles)];
+  float* rinv_s = (float*)(smem + 2 * 65536);
+  float* rs_stage = rinv_s + TBM;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = (M + TBM - 1) / TBM, tiles_n = (N + TBN - 1) / TBN;
+  const int pid = xcd_remap(blockIdx.x, gridDim.x);
+  constexpr int GM = 8;
+  const int grp = pid / (GM * tiles_n);
+  const int first_m = grp * GM;
+  const int gsz = min(tiles_m - first_m, GM);
+  const int in_grp = pid % (GM * tiles_n);
+  const int tm = first_m + in_grp % gsz, tn = in_grp / gsz;
+  const int m0 = tm * TBM, n0 = tn * TBN;
+
+  // DMA: each operand tile is 256 rows x 128 B = 32 instructions of 8 rows; wave w issues row
+  // groups 8w .. 8w + 7 of A and of B.  Lane l of a group lands at row 8g + l / 8, LDS chunk l % 8,
+  // so it loads the global chunk (l % 8) ^ swz2(row) (gemm256_kernel's image)
+  uint32_t src_a[8], src_b[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = (8 * wave + i) * 8 + (lane >> 3);
+    const int ch = ((lane & 7) ^ swz2(r)) * 8;
+    src_a[i] = (uint32_t)min(m0 + r, M - 1) * (uint32_t)K + (uint32_t)ch;
+    src_b[i] = (uint32_t)min(n0 + r, N - 1) * (uint32_t)K + (uint32_t)ch;
+  }
+  // one 1-KiB DMA instruction (i < 8: A row group 8 wave + i, else B), issued where the compiler
+  // cannot see it: with the builtin it waited vmcnt(0) before LDS reads it could not prove disjoint
+  // from the DMA's bytes.  The loop orders the DMA itself (vmcnt + barrier before a buffer is read).
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS_AS char*)smem);
+  auto dma1 = [&](int buf, int k0, int i) {
+    const f16_t* src = i < 8 ? A + src_a[i] + k0 : W + src_b[i - 8] + k0;
+    const uint32_t dst = lds0 + buf * 65536 + (i < 8 ? 0 : 32768) + (8 * wave + (i & 7)) * 8 * 128;
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"{m0}"(dst), "v"(src) : "memory");
+  };
+
+  const int wr = wave >> 1, wc = wave & 1;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int sw = fr >> 1;
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f16x8 af[2][8], bf[2][8];  // [k-step parity][tile]
+  // fragment g of a k-step (g < 8: A tile g, else B tile g - 8) into register set p
+  auto rd1 = [&](int buf, int s, int p, int g) {
+    const char* img = smem + buf * 65536;
+    if (g < 8) af[p][g] = *(const f16x8*)(img + (wr * 128 + g * 16 + fr) * 128 + (((4 * s + fg) ^ sw) << 4));
+    else bf[p][g - 8] = *(const f16x8*)(img + 32768 + (wc * 128 + (g - 8) * 16 + fr) * 128 + (((4 * s + fg) ^ sw) << 4));
+  };
+  // MFMA i (m-major) of register set p, the accumulator pinned in place (AGPRs, "+a"): with the
+  // builtin, hipcc rotated one 4-register tile through a spare AGPR slot every MFMA (184
+  // v_accvgpr_mov per K-tile); dependent MFMAs on one accumulator are interlocked, the reads after
+  // the loop wait below
+  auto mf1 = [&](int p, int i) {
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(af[p][i >> 3]), "v"(bf[p][i & 7]));
+  };
+
+  const int nk = K / TBK;
+  gemm_rs_dma<TBM, 4>(rs, M, m0, rinv_s, rs_stage);
+  f16_t g8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 8; ++ni)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = min(m0 + wr * 128 + mi * 16 + fg * 4 + j, M - 1);
+          const int col = min(n0 + wc * 128 + ni * 16 + fr, N - 1);
+          acc[mi][ni][j] = ((const float*)out)[(size_t)row * ldo + col];
+        }
+    const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
+#pragma unroll
+    for (int ni = 0; ni < 8; ++ni) g8[ni] = gp[min(n0 + wc * 128 + ni * 16 + fr, N - 1)];
+  }
+  // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, its k-step-0 fragments read
+  // (the x preload of the residual epilogue and the statistics DMA are compiler-visible: retired
+  // here, long before the first MFMA)
+  __builtin_amdgcn_s_waitcnt(0);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma1(0, 0, i);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) dma1(1, min(1, nk - 1) * TBK, i);
+  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int g = 0; g < 16; ++g) rd1(0, 0, 0, g);
+  for (int t = 0; t < nk; ++t) {
+    const int cur = t & 1;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): k-step 0's fragments (a builtin: the compiler sees it)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mf1(0, 4 * g);
+      mf1(0, 4 * g + 1);
+      rd1(cur, 1, 1, g);
+      mf1(0, 4 * g + 2);
+      mf1(0, 4 * g + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);                  // lgkmcnt(0): k-step 1's fragments
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // tile t+1 landed (this wave's DMA)
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // ... for every wave: tile t's buffer is free, tile t+1 is in LDS
+    __builtin_amdgcn_s_setprio(1);
+    // (unconditional: past the last tile the DMA re-loads tile nk-1 into the free buffer and the
+    // reads fill the unused register set -- no branches inside the interleave)
+    const int k2 = min(t + 2, nk - 1) * TBK;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mf1(1, 4 * g);
+      dma1(cur, k2, g);
+      mf1(1, 4 * g + 1);
+      rd1(cur ^ 1, 0, 0, g);
+      mf1(1, 4 * g + 2);
+      mf1(1, 4 * g + 3);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  // the last MFMAs' results before any other instruction reads the accumulators (the asm MFMAs
+  // are invisible to the compiler's hazard recognizer)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+  // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x128
+  if constexpr (EPI == 1) {
+    const bool fuse = gr.xg != nullptr;
+    float* red = (float*)smem;
+    if (fuse) __syncthreads();  // every wave is past its K loop: the tile buffers hold the statistics
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float ss[2] = {0.f, 0.f};  // two 64-column halves (gemm256_kernel's wave columns 2wc, 2wc+1)
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+          const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
+          const int col = n0 + wc * 128 + ni * 16 + fr;
+          const float v = acc[mi][ni][j];
+          if (row < M && col < N) {
+            ((float*)out)[(size_t)row * ldo + col] = v;
+            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g8[ni]), ss[ni >> 2]);
+          }
+        }
+        if (fuse)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) red[((wr * 128 + mi * 16 + fg * 4 + j) * 4 + 2 * wc + h) * 16 + fr] = ss[h];
+      }
+    if (fuse) {
+      __syncthreads();
+      for (int q = threadIdx.x; q < TBM * 2; q += blockDim.x) {
+        const int row = q % TBM, g2 = q / TBM;
+        if (m0 + row >= M || n0 + g2 * kGemmStatCols >= N) continue;
+        const float* pp = red + row * 4 * 16 + g2 * 32;
+        float sum = 0.f;
+        for (int k = 0; k < 32; ++k) sum += pp[k];
+        gr.ssq[(size_t)(n0 / kGemmStatCols + g2) * M + m0 + row] = sum;
+      }
+    }
+    return;
+  }
+  gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
+  f32x4 rv4[8];
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) rv4[mi] = f32x4{1.f, 1.f, 1.f, 1.f};
+  if (rs.ssq) {
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) rv4[mi] = *(const f32x4*)(rinv_s + wr * 128 + mi * 16 + fg * 4);
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
+  }
+#pragma unroll
+  for (int mi = 0; mi < 8; ++mi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
+      if (row >= M) continue;
+      const float rv = rv4[mi][j];
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int ni = 0; ni < 8; ni += 2) {
+          const int col = n0 + wc * 128 + ni * 16;
+          if (col >= N) continue;
+          const int f = (col >> 5) * 16 + fr;
+          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
+        }
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < 8; ++ni) {
+          const int col = n0 + wc * 128 + ni * 16 + fr;
+          if (col >= N) continue;
+          const size_t o = (size_t)row * ldo + col;
+          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[mi][ni][j] * rv);
+          else ((float*)out)[o] = acc[mi][ni][j] * rv;
+        }
+      }
+    }
+  }
+}
+
 static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning / tests)
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
 static bool gemm_big(int M, int N) {
-  return g_gemm_variant == 2 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
+  return g_gemm_variant == 2 || g_gemm_variant == 3 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
 }
 
 int gemm_resid_tiles(int M, int N) {
@@ -556,6 +781,16 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
   GemmResid gr{};
   if (gr_in && epi == 1) gr = *gr_in;
 #define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr)
+  if (big && g_gemm_variant == 3 && K % TBK == 0) {
+    const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
+    switch (epi) {
+      case 0: GL(gemm4w_kernel, 0, 256); break;
+      case 1: GL(gemm4w_kernel, 1, 256); break;
+      case 2: GL(gemm4w_kernel, 2, 256); break;
+      default: GL(gemm4w_kernel, 3, 256); break;
+    }
+    return;
+  }
   if (big) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {

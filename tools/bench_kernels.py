@@ -225,7 +225,7 @@ def _trunc(x, bits):
     return (x.view(torch.int16) & ~((1 << bits) - 1)).view(torch.float16)
 
 
-def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0):
+def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=False):
     """rs: the normalised projections (epi 0 / 2) take a one-tile deferred-norm row scale, as
     in prefill (ms_op_set_row_scale; needs a library that has it)"""
     dev = torch.device("cuda:0")
@@ -244,12 +244,27 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0):
             if rs:
                 lib.ms_op_set_row_scale(ssq.data_ptr() if epi in (0, 2) else None, 1, K, 1e-5)
             lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st)
+        ref_out = None
         for variant in variants:
-            lib.ms_set_gemm_variant(variant)
+            L.check(lib.ms_set_gemm_variant(variant))
+            if epi == 1:
+                out.zero_()
+            fn()
+            torch.cuda.synchronize()
+            same = ""
+            if ref_out is None:
+                ref_out = out.clone()
+            else:
+                same = " bit-identical" if torch.equal(out, ref_out) else \
+                    f" DIFFERS (max abs {float((out.float() - ref_out.float()).abs().max()):.3e})"
             t = timeit(fn, reps=5, rounds=3)
+            print(f"  (v{variant} vs v{variants[0]}:{same or ' reference'})", flush=True)
             print(f"gemm v{variant} {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s",
                   flush=True)
         lib.ms_set_gemm_variant(0)
+        if torch_ref:  # the library GEMM (hipBLASLt via torch.matmul) on the same operands, no epilogue
+            t = timeit(lambda: torch.matmul(A, W.t()), reps=5, rounds=3)
+            print(f"torch   {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":
@@ -260,6 +275,7 @@ if __name__ == "__main__":
     ap.add_argument("--trunc", type=int, default=0, help="gemm: clear this many low mantissa bits of A and W")
     ap.add_argument("--rs", action="store_true", help="gemm: deferred-norm row scale on epi 0 / 2")
     ap.add_argument("--variants", default="1,2", help="gemm: tile variants (1: 128x128, 2: 256x256)")
+    ap.add_argument("--torch", action="store_true", help="gemm: also time torch.matmul (hipBLASLt) on the same operands")
     a = ap.parse_args()
     lib = L.load()
     if a.what == "gemv":
@@ -275,4 +291,4 @@ if __name__ == "__main__":
     elif a.what == "camp":
         bench_camp(lib, a.m)
     else:
-        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc)
+        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc, a.torch)
