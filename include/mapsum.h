@@ -190,6 +190,10 @@ int ms_synchronize(ms_engine* e);
 /* diagnostic: the fused QKV + attention launch's phase stamps of its latest launch, [256][16]
    s_memrealtime ticks (100 MHz), recorded only under MS_QA_STAMPS=1 (tools/qa_stamps.py) */
 int ms_debug_qa_stamps(uint64_t* out, int32_t n);
+/* diagnostic: decode attention v2's per-block phase stamps of its latest launch, [1024][24]
+   (entry, XCC / HW id, prologue, per-wave S and P.V done, partial stored), recorded only under
+   MS_A2_STAMPS=1 (tools/a2_stamps.py) */
+int ms_debug_a2_stamps(uint64_t* out, int32_t n);
 
 /* ---- parity probe (tests): one prompt through the prefill path -------------- */
 /* hidden_out: [n][hidden] fp32 residual after `n_layers_run` layers (or NULL);
@@ -229,7 +233,8 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
                      int32_t M, int32_t N, int32_t K, void* stream);
 int ms_gemm_resid_tiles(int32_t M, int32_t N);
 /* tuning/test hook: prefill GEMM tile (0 heuristic, 1 = 128x128, 2 = 256x256 8-phase,
-   3 = 256x256 on 4 waves; bit-identical to 2) */
+   3 = 256x256 on 4 waves, 4 = 3 for the stored epilogues and 2 for the residual one; every
+   variant gives the same bits) */
 int ms_set_gemm_variant(int32_t variant);
 /* tuning/test hook: the K-quant GEMVs that have a grid-stride two-stage form (the Q6_K lm_head
    argmax, the Q4_K gate/up SwiGLU) take it (1, the default) or run one-tile blocks (0); the

@@ -1720,6 +1720,12 @@ int ms_debug_qa_stamps(uint64_t* out, int32_t n) {
   return MS_OK;
 }
 
+int ms_debug_a2_stamps(uint64_t* out, int32_t n) {
+  if (!out || n < 0) return MS_EINVAL;
+  ms::attn2_stamps(reinterpret_cast<unsigned long long*>(out), n);
+  return MS_OK;
+}
+
 int ms_synchronize(ms_engine* e) {
   if (!e) return MS_EINVAL;
   return guarded(e, [&]() -> int {
@@ -1824,6 +1830,8 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
   return op_guard([&] {
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    REQUIRE(epi != MS_EPI_ADD_F32 || (N % 4 == 0 && ldo % 4 == 0), MS_EINVAL,
+            "residual gemm: N and ldo multiples of 4 (16-B x rows)");
     REQUIRE(!g_op_rs.ssq || gemm_rs_tiles_ok(M, N, g_op_rs.tiles), MS_EINVAL,
             "gemm row scale: at most 24 tiles of statistics (kGemmRsTiles, both GEMM tiles)");
     launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
@@ -1836,6 +1844,7 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
     REQUIRE(A && W && x && xg_out && gamma && ssq_out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL,
             "bad gemm_resid operands (K % 64 == 0)");
     REQUIRE(gemm_resid_tiles(M, N) <= kGemmRsTiles, MS_EINVAL, "gemm_resid: N over 24 column tiles");
+    REQUIRE(N % 4 == 0, MS_EINVAL, "gemm_resid: N a multiple of 4 (16-B x rows)");
     GemmResid gr{(const f16_t*)gamma, (f16_t*)xg_out, ssq_out};
     launch_gemm((const f16_t*)A, (const f16_t*)W, x, M, N, K, N, MS_EPI_ADD_F32, (hipStream_t)stream, nullptr, &gr);
   });
@@ -1844,7 +1853,7 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
 int ms_gemm_resid_tiles(int32_t M, int32_t N) { return gemm_resid_tiles(M, N); }
 
 int ms_set_gemm_variant(int32_t v) {
-  if (v < 0 || v > 3) return MS_EINVAL;
+  if (v < 0 || v > 4) return MS_EINVAL;
   set_gemm_variant(v);
   return MS_OK;
 }

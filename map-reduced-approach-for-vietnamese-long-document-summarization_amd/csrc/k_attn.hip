@@ -617,20 +617,35 @@ __global__ __launch_bounds__(256, 2) void attn_decode_kernel(DecodeQKV qa, int H
 // decode step with release / acquire fences (round 2), 2.24 vs 2.13 with write-through stores
 // and one ticket per block (round 4, profiles/r04/v3_attn_fused_combine_rejected_ab.txt): every
 // block's lifetime grows by the drain + ticket round trip.
+// PRE: O values preloaded per thread (>= nsplit where it fits: no redundant loads).  GRP: a
+// 1-D grid whose block L merges (b, kv head) group grp = L % (B * Hk), q head c = L / (B * Hk)
+// of it -- so L % 8 == grp % 8, the XCD of that group's split blocks in launch_attn_decode2's
+// grid (blockIdx = split * B * Hk + grp): the partials are read from the L2 they were written
+// through (plain stores keep the line there; a kernel boundary writes back, it does not evict)
+template <int PRE, bool GRP>
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ ws,
                                                                   f16_t* __restrict__ out, int Hq,
-                                                                  int nsplit) {
+                                                                  int nsplit, int Hk, int B) {
   // one memory round trip: every (m_s, l_s) pair (wave 0, two splits per lane) and, for
-  // nsplit <= 16, every O value of this thread are loaded before the barrier (the O loads
+  // nsplit <= PRE, every O value of this thread are loaded before the barrier (the O loads
   // do not depend on the split weights); sums keep the split order, so results are unchanged
   __shared__ float fw[128], lw[128];
-  const int b = blockIdx.x, hq = blockIdx.y, d = threadIdx.x;
+  int b, hq;
+  if constexpr (GRP) {
+    const int BH = B * Hk, L = blockIdx.x;
+    const int grp = L % BH, c = L / BH;
+    b = grp / Hk;
+    hq = (grp - b * Hk) * (Hq / Hk) + c;
+  } else {
+    b = blockIdx.x;
+    hq = blockIdx.y;
+  }
+  const int d = threadIdx.x;
   const float* p = ws + ((size_t)b * Hq + hq) * nsplit * 132;
   const float* po = p + 2 + d;
-  constexpr int kPre = 16;
-  float ov[kPre];
+  float ov[PRE];
 #pragma unroll
-  for (int q = 0; q < kPre; ++q) ov[q] = po[min(q, nsplit - 1) * 132];
+  for (int q = 0; q < PRE; ++q) ov[q] = q < nsplit ? po[q * 132] : 0.f;
   if (d < 64) {
     const float m0 = d < nsplit ? p[d * 132] : -INFINITY;
     const float m1 = d + 64 < nsplit ? p[(d + 64) * 132] : -INFINITY;
@@ -647,17 +662,41 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
   __syncthreads();
   float L = 0.f, O = 0.f;
 #pragma unroll
-  for (int q = 0; q < kPre; ++q) {
+  for (int q = 0; q < PRE; ++q) {
     if (q < nsplit) {
       L += fw[q] * lw[q];
       O += fw[q] * ov[q];
     }
   }
-  for (int s = kPre; s < nsplit; ++s) {
+  for (int s = PRE; s < nsplit; ++s) {
     L += fw[s] * lw[s];
     O += fw[s] * po[s * 132];
   }
   out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2h(O / L);
+}
+
+// MS_COMBINE_GRP=0: the (B, Hq) grid for v2 too (placement only: the same bits either way)
+static bool combine_grp_ok(int B, int Hk) {
+  static const bool on = [] { const char* e = getenv("MS_COMBINE_GRP"); return !(e && atoi(e) == 0); }();
+  return on && (B * Hk) % 8 == 0;
+}
+
+// the combine launch: (B, Hq) grid, or with grp the 1-D XCD-matched grid of the v2 kernel
+static void launch_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int nsplit, bool grp,
+                           hipStream_t s) {
+#define CB(P_)                                                                                          \
+  do {                                                                                                  \
+    if (grp)                                                                                            \
+      MS_LAUNCH((attn_decode_combine_kernel<P_, true>), dim3(B * Hq), dim3(128), 0, s, ws, out, Hq,     \
+                nsplit, Hk, B);                                                                         \
+    else                                                                                                \
+      MS_LAUNCH((attn_decode_combine_kernel<P_, false>), dim3(B, Hq), dim3(128), 0, s, ws, out, Hq,     \
+                nsplit, Hk, B);                                                                         \
+  } while (0)
+  if (nsplit <= 4) CB(4);
+  else if (nsplit <= 8) CB(8);
+  else CB(16);
+#undef CB
 }
 
 void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView kv,
@@ -682,7 +721,7 @@ void launch_attn_decode(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView 
   if (qa.slabs) AD(true);
   else AD(false);
 #undef AD
-  MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
+  launch_combine(ws, out, a.B, Hq, Hk, nsplit, false, s);
 }
 
 }  // namespace ms
@@ -736,11 +775,24 @@ size_t attn_decode2_workspace_bytes(int B, int Hq, int max_len, int ppb) {
 // the last arriver resets it), with attn_decode_combine_kernel's arithmetic in split order --
 // the same bits as the second launch; the group's blocks share one XCD (blockIdx % 8), so the
 // partials and the counter meet in one L2
+// In-kernel timeline stamps (diagnostic, MS_A2_STAMPS=1, never in a timed run): per block of the
+// latest launch, s_memrealtime (100 MHz) at [0] entry, [2] prologue done, [3 + w] wave w's S done
+// (its K landed), [12 + w] its P.V done, [21] partial stored; [1] = XCC_ID << 16 | HW_ID low half
+// (tools/a2_stamps.py reads them through ms_debug_a2_stamps)
+constexpr int kA2StampBlocks = 1024, kA2Stamps = 24;
+__device__ unsigned long long g_a2_stamps[kA2StampBlocks * kA2Stamps];
+#define A2_STAMP(k)                                                                               \
+  do {                                                                                            \
+    if (stamps && lane == 0 && blockIdx.x < kA2StampBlocks)                                       \
+      stamps[blockIdx.x * kA2Stamps + (k)] = __builtin_amdgcn_s_memrealtime();                    \
+  } while (0)
+
 template <bool FROM_SLABS, int PPB, bool TICKET>
 __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, int Hq, int Hk, KVView kv,
                                                                 DecodeAttnArgs a, float* __restrict__ ws,
                                                                 f16_t* __restrict__ out, int nsplit,
-                                                                float scale_log2, unsigned* __restrict__ cnt) {
+                                                                float scale_log2, unsigned* __restrict__ cnt,
+                                                                unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NTHR = 64 * PPB;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -762,6 +814,14 @@ __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, in
   f16_t* kn = qn + G * kHeadDim;                       // [128] roped k of the new token
   f16_t* vn = kn + kHeadDim;                           // [128] v of the new token
   const bool has_page = pg < np;                       // wave-uniform
+  if (stamps && wave == 0) {
+    A2_STAMP(0);
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && blockIdx.x < kA2StampBlocks)
+      stamps[blockIdx.x * kA2Stamps + 1] = ((unsigned long long)xcc << 32) | hw;
+  }
   // slot-major pool (launch_attn_decode2 checks): page ids are arithmetic, no table load
   const size_t pbase = (((size_t)slot * kv.max_pages + pg) * kv.n_kv_heads + kvh) * kPage * kHeadDim;
 
@@ -867,6 +927,7 @@ __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, in
       kv.v[o] = vn[tid];
     }
   }
+  if (wave == 0) A2_STAMP(2);
 
   // 3. S^T = K Q^T, softmax over the page, O^T = V^T P^T
   f32x4 o[8];
@@ -911,6 +972,7 @@ __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, in
         mx = fmaxf(mx, v);
       }
     mx = grp_max(mx);  // finite: key pg*64 < len is always visible
+    A2_STAMP(3 + wave);
     float rs = 0.f;
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -944,6 +1006,7 @@ __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, in
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
+    A2_STAMP(12 + wave);
   }
   // 4. publish (m, l, O^T) of this wave's 16 columns into its own LDS region, merge in wave order
   {
@@ -981,6 +1044,10 @@ __global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(DecodeQKV qa, in
     } else {
       ws[(((size_t)b * Hq + kvh * G + c) * nsplit + split) * 132 + k] = (k == 0) ? M : acc;
     }
+  }
+  if (stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (wave == 0) A2_STAMP(21);
   }
   if constexpr (TICKET) {
     if (nsplit == 1) return;
@@ -1025,33 +1092,43 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
   const dim3 grid(a.B * Hk * nsplit);
   const size_t lds = attn2_lds_bytes(ppb, Hq / Hk);
+  static unsigned long long* stamps = [] {
+    const char* e = getenv("MS_A2_STAMPS");
+    void* p = nullptr;
+    if (e && atoi(e)) (void)hipGetSymbolAddress(&p, HIP_SYMBOL(g_a2_stamps));
+    return (unsigned long long*)p;
+  }();
 #define A2(P_)                                                                                                \
   case P_:                                                                                                    \
     if (qa.slabs && cnt)                                                                                      \
       MS_LAUNCH((attn_decode2_kernel<true, P_, true>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,    \
-                out, nsplit, scale_log2, cnt);                                                                \
+                out, nsplit, scale_log2, cnt, stamps);                                                        \
     else if (qa.slabs)                                                                                        \
       MS_LAUNCH((attn_decode2_kernel<true, P_, false>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,   \
-                out, nsplit, scale_log2, cnt);                                                                \
+                out, nsplit, scale_log2, cnt, stamps);                                                        \
     else                                                                                                      \
       MS_LAUNCH((attn_decode2_kernel<false, P_, false>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,  \
-                out, nsplit, scale_log2, cnt);                                                                \
+                out, nsplit, scale_log2, cnt, stamps);                                                        \
     break;
   switch (ppb) {
     A2(4) A2(5) A2(6) A2(7) A2(8) A2(9)
     default: return;
   }
 #undef A2
-  if (nsplit > 1 && !(qa.slabs && cnt))
-    MS_LAUNCH(attn_decode_combine_kernel, dim3(a.B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
+  if (nsplit > 1 && !(qa.slabs && cnt)) launch_combine(ws, out, a.B, Hq, Hk, nsplit, combine_grp_ok(a.B, Hk), s);
 }
 
 }  // namespace ms
 
 namespace ms {
 // the split combine as its own launch (the fused QKV + attention kernel writes the same partials)
-void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int nsplit, hipStream_t s) {
+void attn2_stamps(unsigned long long* host, int n) {
+  n = std::min(n, kA2StampBlocks * kA2Stamps);
+  (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_a2_stamps), (size_t)n * sizeof(unsigned long long));
+}
+
+void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int nsplit, hipStream_t s) {
   if (B <= 0 || nsplit <= 1) return;
-  MS_LAUNCH(attn_decode_combine_kernel, dim3(B, Hq), dim3(128), 0, s, ws, out, Hq, nsplit);
+  launch_combine(ws, out, B, Hq, Hk, nsplit, combine_grp_ok(B, Hk), s);
 }
 }  // namespace ms

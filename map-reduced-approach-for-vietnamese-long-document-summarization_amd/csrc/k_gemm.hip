@@ -69,40 +69,41 @@ __device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, 
   }
   __syncthreads();
 }
-// ---- the residual epilogue's outputs for the next normalised projection
-__device__ __forceinline__ void gemm_resid_xg(const GemmResid& gr, size_t o, float v, float g, float& ss) {
-  float p = v * g * kXgScale;  // (kernels.h: the GEMM input pre-scaled by 2^-4, exactly)
-  asm volatile("" : "+v"(p));  // the fp32 product, then one fp16 rounding (no v_fma_mixlo_f16)
-  gr.xg[o] = f2h(p);
-  ss += v * v;
+// ---- the residual epilogue on the transposed accumulator (every GEMM tile; SWAP): a lane holds
+// x[row][c0 .. c0+3] as one f32x4 -- loaded as the accumulators' initial value, stored as one 16-B
+// write, its f16(x*g*2^-4) as one 8-B write (the four fp32 products, then one rounding each, as
+// gemm_resid_xg), and the four squares added into the lane's partial in column order
+__device__ __forceinline__ void gemm_resid_x4(const GemmResid& gr, float* x, size_t o, f32x4 v, const f16_t (&g)[4],
+                                              bool fuse, float& ss) {
+  *(f32x4*)(x + o) = v;
+  if (!fuse) return;
+  float p[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    p[j] = v[j] * h2f(g[j]) * kXgScale;
+    asm volatile("" : "+v"(p[j]));
+  }
+  *(uint2*)(gr.xg + o) = uint2{pack2h(p[0], p[1]), pack2h(p[2], p[3])};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ss += v[j] * v[j];
 }
-// per-row sums of x^2 per 128-column group of the block (the statistics tile: kGemmStatCols,
-// the same on both GEMM tiles, so a row's statistics -- and its deferred-norm scale -- never
-// depend on which tile the packed prompt length picked): lane partials (its NI columns, in
-// order) -> LDS [row][wave column][lane column] -> one thread per (row, group) adds its two
-// wave columns' 32 partials in order.  The tile buffers are free: every wave is past its K loop.
-template <int BM, int WCOLS, int MI>
-__device__ __forceinline__ void gemm_resid_ssq(char* smem, const float (&ss)[MI][4], int wrow0, int wcol,
-                                               int fg, int fr, int M, int N, int m0, int n0, const GemmResid& gr) {
-  static_assert(WCOLS % 2 == 0, "a statistics group is two 64-column wave columns");
-  constexpr int G = WCOLS / 2;
-  float* red = (float*)smem;
+// statistics of the transposed epilogue: per row and 128-column group, 8 lane partials -- the
+// group's two 64-column halves h, in each the 4 lane groups fg (lane group fg of a half holds its
+// columns 16n + 4fg .. +3, n = 0..3, summed in that order) -- added in (h, fg) order by one
+// thread per (row, group).  red: [rows][groups][8] floats (the free tile buffers)
+template <int BM, int GROUPS>
+__device__ __forceinline__ void gemm_resid_ssq_t(float* red, int M, int N, int m0, int n0, const GemmResid& gr) {
   __syncthreads();
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) red[((wrow0 + mi * 16 + fg * 4 + j) * WCOLS + wcol) * 16 + fr] = ss[mi][j];
-  __syncthreads();
-  for (int t = threadIdx.x; t < BM * G; t += blockDim.x) {
+  for (int t = threadIdx.x; t < BM * GROUPS; t += blockDim.x) {
     const int row = t % BM, grp = t / BM;
     if (m0 + row >= M || n0 + grp * kGemmStatCols >= N) continue;
-    const float* p = red + row * WCOLS * 16 + grp * 32;
+    const float* q = red + (row * GROUPS + grp) * 8;
     float sum = 0.f;
-    for (int q = 0; q < 32; ++q) sum += p[q];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += q[k];
     gr.ssq[(size_t)(n0 / kGemmStatCols + grp) * M + m0 + row] = sum;
   }
 }
-
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ A,
                                                      const f16_t* __restrict__ W,
@@ -147,6 +148,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fg = lane >> 4;
+  // SWAP as gemm256_kernel's (the two tiles must give a prompt the same bits: prefill packing
+  // invariance): C^T, 4 consecutive columns of one row per lane
+  constexpr bool SWAP = true;
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -158,21 +162,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
   gemm_rs_dma<GBM, 4>(rs, M, m0, rinv_s, rs_stage);
   // residual epilogue: x as the accumulators' initial value (as gemm256_kernel)
-  f16_t g4[4] = {0, 0, 0, 0};  // raw bits, converted in the epilogue
+  f16_t g4[4][4] = {};  // raw bits, converted in the epilogue
   if constexpr (EPI == 1) {
+    // transposed: acc[m][n] = x[row 16m + fr][cols 16n + 4fg .. +3], one 16-B load each
 #pragma unroll
     for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = min(m0 + wm * 64 + m * 16 + fg * 4 + j, M - 1);
-          const int col = min(n0 + wn * 64 + n * 16 + fr, N - 1);
-          acc[m][n][j] = ((const float*)out)[(size_t)row * ldo + col];
-        }
+      for (int n = 0; n < 4; ++n) {
+        const int row = min(m0 + wm * 64 + m * 16 + fr, M - 1);
+        const int col = min(n0 + wn * 64 + n * 16 + 4 * fg, N - 4);
+        acc[m][n] = *(const f32x4*)((const float*)out + (size_t)row * ldo + col);
+      }
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;  // unconditional load (no merge wait)
 #pragma unroll
-    for (int n = 0; n < 4; ++n) g4[n] = gp[min(n0 + wn * 64 + n * 16 + fr, N - 1)];
+    for (int n = 0; n < 4; ++n) {
+      const uint2 w = *(const uint2*)(gp + min(n0 + wn * 64 + n * 16 + 4 * fg, N - 4));
+      g4[n][0] = (f16_t)(w.x & 0xFFFF); g4[n][1] = (f16_t)(w.x >> 16);
+      g4[n][2] = (f16_t)(w.y & 0xFFFF); g4[n][3] = (f16_t)(w.y >> 16);
+    }
   }
   stage(0, 0);
   wait_vmcnt0();
@@ -200,34 +207,87 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 #pragma unroll
       for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(af[m], bfr[n], acc[m][n]);
+        for (int n = 0; n < 4; ++n)
+          acc[m][n] = SWAP ? mfma16(bfr[n], af[m], acc[m][n]) : mfma16(af[m], bfr[n], acc[m][n]);
     }
     wait_vmcnt0();
     __syncthreads();
   }
 
-  // epilogue: acc[m][n][j] = C[row 4*fg + j][col fr] of 16x16 tile (m, n)
+  // epilogue: acc[m][n][j] = C[row 16m + fr][col 16n + 4fg + j] of the wave's 64x64
   if constexpr (EPI == 1) {  // residual add (x was the accumulators' initial value)
     const bool fuse = gr.xg != nullptr;
-    float ss[4][4] = {};
+    float* red = (float*)smem;
+    if (fuse) __syncthreads();  // every wave is past its K loop: the tile buffers are free
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int m = 0; m < 4; ++m) {
+      const int row = m0 + wm * 64 + m * 16 + fr;
+      float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
-          const int col = n0 + wn * 64 + n * 16 + fr;
-          const float v = acc[m][n][j];
-          if (row < M && col < N) {
-            ((float*)out)[(size_t)row * ldo + col] = v;
-            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g4[n]), ss[m][j]);
-          }
-        }
-    if (fuse) gemm_resid_ssq<GBM, 2, 4>(smem, ss, wm * 64, wn, fg, fr, M, N, m0, n0, gr);
+      for (int n = 0; n < 4; ++n) {
+        const int col = n0 + wn * 64 + n * 16 + 4 * fg;
+        if (row < M && col < N) gemm_resid_x4(gr, (float*)out, (size_t)row * ldo + col, acc[m][n], g4[n], fuse, ss);
+      }
+      if (fuse) red[(wm * 64 + m * 16 + fr) * 8 + wn * 4 + fg] = ss;
+    }
+    if (fuse) gemm_resid_ssq_t<GBM, 1>(red, M, N, m0, n0, gr);
     return;
   }
   gemm_rs_fold<GBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
+  if constexpr (SWAP) {
+    // acc[m][n][j] = C[row 16m + fr][col 16n + 4fg + j] of the wave's 64x64
+    float rv[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) rv[m] = 1.f;
+    if (rs.ssq) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) rv[m] = rs_rinv(rinv_s[wm * 64 + m * 16 + fr], rs);
+    }
+    const bool vec = (ldo & 3) == 0;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int row = m0 + wm * 64 + m * 16 + fr;
+      if (row >= M) continue;
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int n = 0; n < 4; n += 2) {
+          const int col = n0 + wn * 64 + n * 16;
+          if (col >= N) continue;
+          const int f = (col >> 5) * 16 + 4 * fg;
+          float hv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hv[j] = silu_mul(acc[m][n][j] * rv[m], acc[m][n + 1][j] * rv[m]);
+          f16_t* o = (f16_t*)out + (size_t)row * ldo + f;
+          if (vec) {
+            *(uint2*)o = uint2{pack2h(hv[0], hv[1]), pack2h(hv[2], hv[3])};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2h(hv[j]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int col = n0 + wn * 64 + n * 16 + 4 * fg;
+          if (col >= N) continue;
+          const size_t o = (size_t)row * ldo + col;
+          const f32x4 v = acc[m][n] * rv[m];
+          if (vec && col + 3 < N) {
+            if constexpr (EPI == 0) *(uint2*)((f16_t*)out + o) = uint2{pack2h(v[0], v[1]), pack2h(v[2], v[3])};
+            else *(f32x4*)((float*)out + o) = v;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (col + j < N) {
+                if constexpr (EPI == 0) ((f16_t*)out)[o + j] = f2h(v[j]);
+                else ((float*)out)[o + j] = v[j];
+              }
+          }
+        }
+      }
+    }
+    return;
+  }
   f32x4 rv4[4];  // the rows' norm factors, as gemm256_kernel's epilogue
 #pragma unroll
   for (int m = 0; m < 4; ++m) rv4[m] = f32x4{1.f, 1.f, 1.f, 1.f};
@@ -350,6 +410,10 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fg = lane >> 4;
   const int sw = fr >> 1;  // swz2(row) for every fragment row (rows = 16-aligned base + fr)
+  // SWAP: the MFMA computes C^T (W fragment as the A operand), so a lane holds 4 CONSECUTIVE
+  // columns of one row -- the epilogues load / store 8 / 16 B per lane instead of one 2 / 4-B
+  // element (the swapped MFMA can round differently in the last bit: every GEMM tile swaps)
+  constexpr bool SWAP = true;
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -388,7 +452,8 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          acc[qa * 4 + m][qb * 2 + n] = mfma16(af[m][s2], bfr[n][s2], acc[qa * 4 + m][qb * 2 + n]);
+          acc[qa * 4 + m][qb * 2 + n] = SWAP ? mfma16(bfr[n][s2], af[m][s2], acc[qa * 4 + m][qb * 2 + n])
+                                             : mfma16(af[m][s2], bfr[n][s2], acc[qa * 4 + m][qb * 2 + n]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -400,22 +465,25 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   // residual epilogue: the tile's x is the accumulators' initial value, loaded ahead of the
   // first K tile (the prologue's vmcnt waits retire it with tile 0), so the MFMAs add A . W^T
   // onto x and the epilogue only stores -- no load round trips after the K loop
-  f16_t g4[4] = {0, 0, 0, 0};  // raw bits: converted in the epilogue (a conversion here waited)
+  f16_t g4[4][4] = {};  // raw bits: converted in the epilogue (a conversion here waited)
   if constexpr (EPI == 1) {
+    // transposed: acc[mi][ni] = x[row 16mi + fr][cols 16ni + 4fg .. +3], one 16-B load each
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = min(m0 + wr * 128 + mi * 16 + fg * 4 + j, M - 1);
-          const int col = min(n0 + wc * 64 + ni * 16 + fr, N - 1);
-          acc[mi][ni][j] = ((const float*)out)[(size_t)row * ldo + col];
-        }
+      for (int ni = 0; ni < 4; ++ni) {
+        const int row = min(m0 + wr * 128 + mi * 16 + fr, M - 1);
+        const int col = min(n0 + wc * 64 + ni * 16 + 4 * fg, N - 4);
+        acc[mi][ni] = *(const f32x4*)((const float*)out + (size_t)row * ldo + col);
+      }
     // unconditional (a conditional load's merge made the wave wait for it right here)
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) g4[ni] = gp[min(n0 + wc * 64 + ni * 16 + fr, N - 1)];
+    for (int ni = 0; ni < 4; ++ni) {
+      const uint2 w = *(const uint2*)(gp + min(n0 + wc * 64 + ni * 16 + 4 * fg, N - 4));
+      g4[ni][0] = (f16_t)(w.x & 0xFFFF); g4[ni][1] = (f16_t)(w.x >> 16);
+      g4[ni][2] = (f16_t)(w.y & 0xFFFF); g4[ni][3] = (f16_t)(w.y >> 16);
+    }
   }
   // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
   stage(0, 0, 0);
@@ -463,30 +531,85 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   }
   if (wr == 0) __builtin_amdgcn_s_barrier();  // balance the stagger
 
-  // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x64
+  // epilogue: acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x64
   if constexpr (EPI == 1) {
     // residual add (x was the accumulators' initial value): store x, and with gr.xg also the
     // next projection's input and its statistics
     const bool fuse = gr.xg != nullptr;
-    float ss[8][4] = {};
+    float* red = (float*)smem;
+    if (fuse) __syncthreads();  // every wave is past its K loop: the tile buffers are free
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int mi = 0; mi < 8; ++mi) {
+      const int row = m0 + wr * 128 + mi * 16 + fr;
+      float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
-          const int col = n0 + wc * 64 + ni * 16 + fr;
-          const float v = acc[mi][ni][j];
-          if (row < M && col < N) {
-            ((float*)out)[(size_t)row * ldo + col] = v;
-            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g4[ni]), ss[mi][j]);
-          }
-        }
-    if (fuse) gemm_resid_ssq<TBM, 4, 8>(smem, ss, wr * 128, wc, fg, fr, M, N, m0, n0, gr);
+      for (int ni = 0; ni < 4; ++ni) {
+        const int col = n0 + wc * 64 + ni * 16 + 4 * fg;
+        if (row < M && col < N) gemm_resid_x4(gr, (float*)out, (size_t)row * ldo + col, acc[mi][ni], g4[ni], fuse, ss);
+      }
+      if (fuse) red[((wr * 128 + mi * 16 + fr) * 2 + (wc >> 1)) * 8 + (wc & 1) * 4 + fg] = ss;
+    }
+    if (fuse) gemm_resid_ssq_t<TBM, 2>(red, M, N, m0, n0, gr);
     return;
   }
   gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
+  if constexpr (SWAP) {
+    // acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x64: one row factor
+    // per mi, the four columns of a (mi, ni) stored as one 8-B (fp16) / 16-B (fp32) write
+    float rv[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) rv[mi] = 1.f;
+    if (rs.ssq) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rv[mi] = rinv_s[wr * 128 + mi * 16 + fr];
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rv[mi] = rs_rinv(rv[mi], rs);
+    }
+    const bool vec = (ldo & 3) == 0;  // block-uniform: 4-element groups stay aligned
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int row = m0 + wr * 128 + mi * 16 + fr;
+      if (row >= M) continue;
+      if constexpr (EPI == 2) {  // SwiGLU: ni even = gate, ni odd = up of the same 16 features
+#pragma unroll
+        for (int ni = 0; ni < 4; ni += 2) {
+          const int col = n0 + wc * 64 + ni * 16;  // multiple of 32
+          if (col >= N) continue;
+          const int f = (col >> 5) * 16 + 4 * fg;
+          float hv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hv[j] = silu_mul(acc[mi][ni][j] * rv[mi], acc[mi][ni + 1][j] * rv[mi]);
+          f16_t* o = (f16_t*)out + (size_t)row * ldo + f;
+          if (vec) {
+            *(uint2*)o = uint2{pack2h(hv[0], hv[1]), pack2h(hv[2], hv[3])};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2h(hv[j]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int col = n0 + wc * 64 + ni * 16 + 4 * fg;
+          if (col >= N) continue;
+          const size_t o = (size_t)row * ldo + col;
+          const f32x4 v = acc[mi][ni] * rv[mi];
+          if (vec && col + 3 < N) {
+            if constexpr (EPI == 0) *(uint2*)((f16_t*)out + o) = uint2{pack2h(v[0], v[1]), pack2h(v[2], v[3])};
+            else *(f32x4*)((float*)out + o) = v;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (col + j < N) {
+                if constexpr (EPI == 0) ((f16_t*)out)[o + j] = f2h(v[j]);
+                else ((float*)out)[o + j] = v[j];
+              }
+          }
+        }
+      }
+    }
+    return;
+  }
   // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
   // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
   // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
@@ -606,27 +729,34 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
   // builtin, hipcc rotated one 4-register tile through a spare AGPR slot every MFMA (184
   // v_accvgpr_mov per K-tile); dependent MFMAs on one accumulator are interlocked, the reads after
   // the loop wait below
+  // SWAP (gemm256_kernel's): C^T, 4 consecutive columns of one row per lane
+  constexpr bool SWAP = true;
   auto mf1 = [&](int p, int i) {
-    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(af[p][i >> 3]), "v"(bf[p][i & 7]));
+    if constexpr (SWAP)
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(bf[p][i & 7]), "v"(af[p][i >> 3]));
+    else
+      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(af[p][i >> 3]), "v"(bf[p][i & 7]));
   };
 
   const int nk = K / TBK;
   gemm_rs_dma<TBM, 4>(rs, M, m0, rinv_s, rs_stage);
-  f16_t g8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  f16_t g8[8][4] = {};
   if constexpr (EPI == 1) {
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 8; ++ni)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = min(m0 + wr * 128 + mi * 16 + fg * 4 + j, M - 1);
-          const int col = min(n0 + wc * 128 + ni * 16 + fr, N - 1);
-          acc[mi][ni][j] = ((const float*)out)[(size_t)row * ldo + col];
-        }
+      for (int ni = 0; ni < 8; ++ni) {
+        const int row = min(m0 + wr * 128 + mi * 16 + fr, M - 1);
+        const int col = min(n0 + wc * 128 + ni * 16 + 4 * fg, N - 4);
+        acc[mi][ni] = *(const f32x4*)((const float*)out + (size_t)row * ldo + col);
+      }
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
 #pragma unroll
-    for (int ni = 0; ni < 8; ++ni) g8[ni] = gp[min(n0 + wc * 128 + ni * 16 + fr, N - 1)];
+    for (int ni = 0; ni < 8; ++ni) {
+      const uint2 w = *(const uint2*)(gp + min(n0 + wc * 128 + ni * 16 + 4 * fg, N - 4));
+      g8[ni][0] = (f16_t)(w.x & 0xFFFF); g8[ni][1] = (f16_t)(w.x >> 16);
+      g8[ni][2] = (f16_t)(w.y & 0xFFFF); g8[ni][3] = (f16_t)(w.y >> 16);
+    }
   }
   // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, its k-step-0 fragments read
   // (the x preload of the residual epilogue and the statistics DMA are compiler-visible: retired
@@ -678,44 +808,83 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
   // are invisible to the compiler's hazard recognizer)
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
 
-  // epilogue: acc[mi][ni][j] = C[row 16mi + 4fg + j][col 16ni + fr] of the wave's 128x128
+  // epilogue: acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x128
   if constexpr (EPI == 1) {
     const bool fuse = gr.xg != nullptr;
     float* red = (float*)smem;
     if (fuse) __syncthreads();  // every wave is past its K loop: the tile buffers hold the statistics
 #pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
+    for (int mi = 0; mi < 8; ++mi) {
+      const int row = m0 + wr * 128 + mi * 16 + fr;
+      float ss[2] = {0.f, 0.f};  // two 64-column halves (gemm256_kernel's wave columns 2wc, 2wc+1)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float ss[2] = {0.f, 0.f};  // two 64-column halves (gemm256_kernel's wave columns 2wc, 2wc+1)
+      for (int ni = 0; ni < 8; ++ni) {
+        const int col = n0 + wc * 128 + ni * 16 + 4 * fg;
+        if (row < M && col < N)
+          gemm_resid_x4(gr, (float*)out, (size_t)row * ldo + col, acc[mi][ni], g8[ni], fuse, ss[ni >> 2]);
+      }
+      if (fuse)
 #pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
-          const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
-          const int col = n0 + wc * 128 + ni * 16 + fr;
-          const float v = acc[mi][ni][j];
-          if (row < M && col < N) {
-            ((float*)out)[(size_t)row * ldo + col] = v;
-            if (fuse) gemm_resid_xg(gr, (size_t)row * ldo + col, v, h2f(g8[ni]), ss[ni >> 2]);
+        for (int h = 0; h < 2; ++h) red[((wr * 128 + mi * 16 + fr) * 2 + wc) * 8 + h * 4 + fg] = ss[h];
+    }
+    if (fuse) gemm_resid_ssq_t<TBM, 2>(red, M, N, m0, n0, gr);
+    return;
+  }
+  gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
+  if constexpr (SWAP) {
+    // acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x128
+    float rv[8];
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) rv[mi] = 1.f;
+    if (rs.ssq) {
+#pragma unroll
+      for (int mi = 0; mi < 8; ++mi) rv[mi] = rs_rinv(rinv_s[wr * 128 + mi * 16 + fr], rs);
+    }
+    const bool vec = (ldo & 3) == 0;
+#pragma unroll
+    for (int mi = 0; mi < 8; ++mi) {
+      const int row = m0 + wr * 128 + mi * 16 + fr;
+      if (row >= M) continue;
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int ni = 0; ni < 8; ni += 2) {
+          const int col = n0 + wc * 128 + ni * 16;
+          if (col >= N) continue;
+          const int f = (col >> 5) * 16 + 4 * fg;
+          float hv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) hv[j] = silu_mul(acc[mi][ni][j] * rv[mi], acc[mi][ni + 1][j] * rv[mi]);
+          f16_t* o = (f16_t*)out + (size_t)row * ldo + f;
+          if (vec) {
+            *(uint2*)o = uint2{pack2h(hv[0], hv[1]), pack2h(hv[2], hv[3])};
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = f2h(hv[j]);
           }
         }
-        if (fuse)
+      } else {
 #pragma unroll
-          for (int h = 0; h < 2; ++h) red[((wr * 128 + mi * 16 + fg * 4 + j) * 4 + 2 * wc + h) * 16 + fr] = ss[h];
-      }
-    if (fuse) {
-      __syncthreads();
-      for (int q = threadIdx.x; q < TBM * 2; q += blockDim.x) {
-        const int row = q % TBM, g2 = q / TBM;
-        if (m0 + row >= M || n0 + g2 * kGemmStatCols >= N) continue;
-        const float* pp = red + row * 4 * 16 + g2 * 32;
-        float sum = 0.f;
-        for (int k = 0; k < 32; ++k) sum += pp[k];
-        gr.ssq[(size_t)(n0 / kGemmStatCols + g2) * M + m0 + row] = sum;
+        for (int ni = 0; ni < 8; ++ni) {
+          const int col = n0 + wc * 128 + ni * 16 + 4 * fg;
+          if (col >= N) continue;
+          const size_t o = (size_t)row * ldo + col;
+          const f32x4 v = acc[mi][ni] * rv[mi];
+          if (vec && col + 3 < N) {
+            if constexpr (EPI == 0) *(uint2*)((f16_t*)out + o) = uint2{pack2h(v[0], v[1]), pack2h(v[2], v[3])};
+            else *(f32x4*)((float*)out + o) = v;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              if (col + j < N) {
+                if constexpr (EPI == 0) ((f16_t*)out)[o + j] = f2h(v[j]);
+                else ((float*)out)[o + j] = v[j];
+              }
+          }
+        }
       }
     }
     return;
   }
-  gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
   f32x4 rv4[8];
 #pragma unroll
   for (int mi = 0; mi < 8; ++mi) rv4[mi] = f32x4{1.f, 1.f, 1.f, 1.f};
@@ -756,12 +925,18 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
   }
 }
 
-static int g_gemm_variant = 0;  // 0: heuristic, 1: 128x128, 2: 256x256 (tuning / tests)
+// 0: heuristic (8-wave big tile), 1: 128x128, 2: 256x256 8-wave, 3: 256x256 4-wave, 4 (default):
+// the heuristic with the 4-wave kernel for the stored epilogues and the 8-wave one for the residual
+// epilogue (the 4-wave residual form spills) -- QKV 437 -> 422 us, gate/up 1327 -> 1321 us per
+// launch, prefill 87.0 -> 86.2 ms per configs[1] step (profiles/r05/v11_*).  Tests and sweeps set
+// it (ms_set_gemm_variant, MS_GEMM_VARIANT); every variant gives the same bits
+static int g_gemm_variant = [] { const char* e = getenv("MS_GEMM_VARIANT"); return e ? atoi(e) : 4; }();
 
 void set_gemm_variant(int v) { g_gemm_variant = v; }
 
 static bool gemm_big(int M, int N) {
-  return g_gemm_variant == 2 || g_gemm_variant == 3 || (g_gemm_variant == 0 && M >= 1024 && N >= 1024);
+  return g_gemm_variant == 2 || g_gemm_variant == 3 ||
+         ((g_gemm_variant == 0 || g_gemm_variant == 4) && M >= 1024 && N >= 1024);
 }
 
 int gemm_resid_tiles(int M, int N) {
@@ -781,7 +956,7 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
   GemmResid gr{};
   if (gr_in && epi == 1) gr = *gr_in;
 #define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr)
-  if (big && g_gemm_variant == 3 && K % TBK == 0) {
+  if (big && (g_gemm_variant == 3 || (g_gemm_variant == 4 && epi != 1)) && K % TBK == 0) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {
       case 0: GL(gemm4w_kernel, 0, 256); break;

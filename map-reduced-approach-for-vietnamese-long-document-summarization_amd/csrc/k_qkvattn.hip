@@ -506,7 +506,7 @@ void launch_qkv_attn(const f16_t* xb, const f16_t* wqkv, float* qkv32, const Dec
 #define QL(P_) case P_: MS_LAUNCH(qkv_attn_kernel<P_>, dim3(kQaBlocks), dim3(kQaThreads), lds, s, a); break;
   switch (ppb) { QL(4) QL(5) QL(6) QL(7) QL(8) QL(9) default: return; }
 #undef QL
-  launch_attn_combine(ws, out, da.B, Hq, a.nsplit, s);
+  launch_attn_combine(ws, out, da.B, Hq, Hk, a.nsplit, s);
 }
 
 void qkv_attn_stamps(unsigned long long* host, int n) {

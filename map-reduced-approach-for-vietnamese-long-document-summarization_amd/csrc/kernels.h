@@ -275,7 +275,7 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
                          float* ws, int ppb, hipStream_t s, unsigned* cnt = nullptr);
 
 // merge nsplit decode-attention partials (launch_attn_decode2's workspace layout) into out
-void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int nsplit, hipStream_t s);
+void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int nsplit, hipStream_t s);
 
 // The decode step's QKV projection and attention as ONE launch (k_qkvattn.hip): 256 workgroups
 // (one per CU, all resident) each compute 20 rows of the QKV projection -- bit-identical to the
@@ -286,6 +286,8 @@ void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int nsplit,
 bool qkv_attn_supported(int B, int max_batch, int H, int Hq, int Hk, int max_len, int ppb, int split_qkv);
 // diagnostic: the latest launch's phase stamps [256][16] (MS_QA_STAMPS=1), 100 MHz ticks
 void qkv_attn_stamps(unsigned long long* host, int n);
+// decode attention v2's per-block phase stamps of its latest launch (MS_A2_STAMPS=1), [1024][24]
+void attn2_stamps(unsigned long long* host, int n);
 void launch_qkv_attn(const f16_t* xb, const f16_t* wqkv, float* qkv32, const DecodeQKV& qa, f16_t* out, int Hq,
                      int Hk, KVView kv, DecodeAttnArgs a, float* ws, int ppb, unsigned* sync, unsigned* err,
                      hipStream_t s);

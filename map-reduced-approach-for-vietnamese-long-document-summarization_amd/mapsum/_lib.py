@@ -21,6 +21,8 @@ MS_FLAG_IGNORE_EOS = 1
  MS_T_WUP, MS_T_WDOWN, MS_T_FINAL_NORM, MS_T_LM_HEAD) = range(12)
 MS_EPI_STORE_F16, MS_EPI_ADD_F32, MS_EPI_SWIGLU, MS_EPI_STORE_F32 = range(4)
 MS_EPI_ARGMAX = 5
+# the prefill GEMM dispatch the library starts with (ms_set_gemm_variant; tests restore it)
+GEMM_DEFAULT = 4
 MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms
 K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC, K_QKV_ATTN = range(7)
@@ -35,7 +37,7 @@ EXPORTED = (
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
     "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
-    "ms_trace_push", "ms_trace_pop", "ms_debug_qa_stamps",
+    "ms_trace_push", "ms_trace_pop", "ms_debug_qa_stamps", "ms_debug_a2_stamps",
 )
 
 
@@ -76,7 +78,14 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libmapsum.so not found at {LIB_PATH}; build it with "
                            f"`make -C csrc` or `python -c 'import __graft_entry__ as g; g.build()'`")
-    lib = C.CDLL(LIB_PATH)
+    _lib = load_at(LIB_PATH, bool(os.environ.get("MAPSUM_LIB")))
+    return _lib
+
+
+def load_at(path: str, ab: bool = True) -> C.CDLL:
+    """A build of the library at `path` with the C-ABI signatures set (tools: same-process A/B
+    of two builds; ab: tolerate entry points an older build lacks)."""
+    lib = C.CDLL(path)
     vp, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
     pi32 = C.POINTER(C.c_int32)
     sig = {
@@ -126,15 +135,14 @@ def load() -> C.CDLL:
         "ms_trace_push": (i32, [C.c_char_p]),
         "ms_trace_pop": (i32, []),
         "ms_debug_qa_stamps": (i32, [vp, i32]),
+        "ms_debug_a2_stamps": (i32, [vp, i32]),
     }
-    ab = bool(os.environ.get("MAPSUM_LIB"))  # an A/B build may predate the newest op hooks
     for name, (res, args) in sig.items():
-        if ab and not hasattr(lib, name):
+        if ab and not hasattr(lib, name):  # an A/B build may predate the newest op hooks
             continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
     return lib
 
 

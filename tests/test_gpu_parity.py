@@ -97,7 +97,7 @@ def test_gemm_epilogues(lib, dev, M, N, K, epi, variant):
         L.check(lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, _stream()))
         torch.cuda.synchronize()
     finally:
-        lib.ms_set_gemm_variant(0)
+        lib.ms_set_gemm_variant(L.GEMM_DEFAULT)
     if epi == L.MS_EPI_STORE_F16:
         exp, tol = ref, 4e-3
     elif epi == L.MS_EPI_ADD_F32:
@@ -342,7 +342,7 @@ def test_gemm_4wave_bit_exact(lib, dev, M, N, K, epi):
             torch.cuda.synchronize()
             outs.append((out,))
         finally:
-            L.check(lib.ms_set_gemm_variant(0))
+            L.check(lib.ms_set_gemm_variant(L.GEMM_DEFAULT))
     for a, b in zip(outs[0], outs[1]):
         assert torch.equal(a, b)
 
@@ -386,7 +386,7 @@ def test_gemm_resid_epilogue(lib, dev, M, variant):
             L.check(lib.ms_op_set_row_scale(None, 0, 0, 0.0))
         torch.cuda.synchronize()
     finally:
-        L.check(lib.ms_set_gemm_variant(0))
+        L.check(lib.ms_set_gemm_variant(L.GEMM_DEFAULT))
     xd = x.double().cpu()
     r = XG_UNSCALE / torch.sqrt((xd * xd).mean(-1, keepdim=True) + eps)
     exp = r * (xg.double().cpu() @ Wq.double().cpu().T)

@@ -225,9 +225,10 @@ def _trunc(x, bits):
     return (x.view(torch.int16) & ~((1 << bits) - 1)).view(torch.float16)
 
 
-def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=False):
+def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=False, ref_lib=None, resid=False):
     """rs: the normalised projections (epi 0 / 2) take a one-tile deferred-norm row scale, as
-    in prefill (ms_op_set_row_scale; needs a library that has it)"""
+    in prefill (ms_op_set_row_scale; needs a library that has it).  ref_lib: a second build
+    (L.load_at) timed on the same operands right after each variant, and checked bit for bit"""
     dev = torch.device("cuda:0")
     st = torch.cuda.current_stream().cuda_stream
     ssq = (torch.rand(16384, device=dev) * 3072 + 1.0).float()
@@ -239,11 +240,23 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=Fa
         out = torch.zeros(M, N if epi != 2 else N // 2, device=dev,
                           dtype=torch.float32 if epi in (1, 3) else torch.float16)
         ldo = N if epi != 2 else N // 2
+        # the engine's residual form (--resid): x += A W^T, f16(x g 2^-4) and the 128-column
+        # statistics (ms_op_gemm_resid) instead of the plain add
+        xg = torch.empty(M, N, device=dev, dtype=torch.float16) if resid and epi == 1 else None
+        gam = torch.rand(N, device=dev).to(torch.float16) if xg is not None else None
+        sq = torch.empty(N // 128, M, device=dev) if xg is not None else None
+
+        def call(L_, o_):
+            if xg is not None:
+                L_.ms_op_gemm_resid(A.data_ptr(), W.data_ptr(), o_.data_ptr(), xg.data_ptr(), gam.data_ptr(),
+                                    sq.data_ptr(), M, N, K, st)
+            else:
+                L_.ms_op_gemm(A.data_ptr(), W.data_ptr(), o_.data_ptr(), M, N, K, ldo, epi, st)
 
         def fn():
             if rs:
                 lib.ms_op_set_row_scale(ssq.data_ptr() if epi in (0, 2) else None, 1, K, 1e-5)
-            lib.ms_op_gemm(A.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st)
+            call(lib, out)
         ref_out = None
         for variant in variants:
             L.check(lib.ms_set_gemm_variant(variant))
@@ -261,7 +274,30 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=Fa
             print(f"  (v{variant} vs v{variants[0]}:{same or ' reference'})", flush=True)
             print(f"gemm v{variant} {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s",
                   flush=True)
-        lib.ms_set_gemm_variant(0)
+            if ref_lib is not None:
+                mine = out.clone()
+
+                def fn_ref():
+                    if rs:
+                        ref_lib.ms_op_set_row_scale(ssq.data_ptr() if epi in (0, 2) else None, 1, K, 1e-5)
+                    call(ref_lib, out)
+                L.check(ref_lib.ms_set_gemm_variant(variant))
+                if epi == 1:  # the residual epilogue accumulates: compare one launch on zeros each
+                    out.zero_()
+                    fn()
+                    torch.cuda.synchronize()
+                    mine = out.clone()
+                    out.zero_()
+                fn_ref()
+                torch.cuda.synchronize()
+                eq = "bit-identical" if torch.equal(out, mine) else \
+                    f"DIFFERS (max abs {float((out.float() - mine.float()).abs().max()):.3e})"
+                tr = timeit(fn_ref, reps=5, rounds=3)
+                t2 = timeit(fn, reps=5, rounds=3)
+                print(f"base v{variant} {name:5s} M={M} N={N} K={K}: {tr:.3f} ms  {2*M*N*K/tr/1e9:.0f} TFLOP/s "
+                      f"(this build again {t2:.3f} ms; outputs {eq})", flush=True)
+                ref_lib.ms_set_gemm_variant(4)
+        lib.ms_set_gemm_variant(L.GEMM_DEFAULT)
         if torch_ref:  # the library GEMM (hipBLASLt via torch.matmul) on the same operands, no epilogue
             t = timeit(lambda: torch.matmul(A, W.t()), reps=5, rounds=3)
             print(f"torch   {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s", flush=True)
@@ -276,6 +312,8 @@ if __name__ == "__main__":
     ap.add_argument("--rs", action="store_true", help="gemm: deferred-norm row scale on epi 0 / 2")
     ap.add_argument("--variants", default="1,2", help="gemm: tile variants (1: 128x128, 2: 256x256)")
     ap.add_argument("--torch", action="store_true", help="gemm: also time torch.matmul (hipBLASLt) on the same operands")
+    ap.add_argument("--ref-lib", default="", help="gemm: a second build (e.g. libmapsum_base.so) timed and compared")
+    ap.add_argument("--resid", action="store_true", help="gemm: O / down through ms_op_gemm_resid (the engine's form)")
     a = ap.parse_args()
     lib = L.load()
     if a.what == "gemv":
@@ -291,4 +329,5 @@ if __name__ == "__main__":
     elif a.what == "camp":
         bench_camp(lib, a.m)
     else:
-        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc, a.torch)
+        ref = L.load_at(a.ref_lib) if a.ref_lib else None
+        bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc, a.torch, ref, a.resid)
