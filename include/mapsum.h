@@ -190,7 +190,7 @@ int ms_synchronize(ms_engine* e);
 /* diagnostic: the fused QKV + attention launch's phase stamps of its latest launch, [256][16]
    s_memrealtime ticks (100 MHz), recorded only under MS_QA_STAMPS=1 (tools/qa_stamps.py) */
 int ms_debug_qa_stamps(uint64_t* out, int32_t n);
-/* diagnostic: decode attention v2's per-block phase stamps of its latest launch, [1024][24]
+/* diagnostic: decode attention v2's per-block phase stamps of its latest launch, [1024][32]
    (entry, XCC / HW id, prologue, per-wave S and P.V done, partial stored), recorded only under
    MS_A2_STAMPS=1 (tools/a2_stamps.py) */
 int ms_debug_a2_stamps(uint64_t* out, int32_t n);

@@ -29,7 +29,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-__device__ __forceinline__ float silu_mul(float g, float u) { return g / (1.0f + __expf(-g)) * u; }
+// SwiGLU of the prefill epilogues: silu(g) u with v_rcp_f32 (1 ulp) for the division -- the
+// correctly rounded fp32 division's ~10-instruction sequence per element made the gate/up
+// epilogue a visible share of the GEMM (128 elements per lane at one wave per SIMD)
+__device__ __forceinline__ float silu_mul(float g, float u) {
+  return g * __builtin_amdgcn_rcpf(1.0f + __expf(-g)) * u;
+}
 
 // ---- deferred-norm statistics of the consumers (epilogues 0, 2, 3).  One tile: the rows' sums
 // of squares by LDS DMA straight into rinv_s; more (a residual epilogue's per-column-tile
@@ -69,7 +74,7 @@ __device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, 
   }
   __syncthreads();
 }
-// ---- the residual epilogue on the transposed accumulator (every GEMM tile; SWAP): a lane holds
+// ---- the residual epilogue on the transposed accumulator (every GEMM tile): a lane holds
 // x[row][c0 .. c0+3] as one f32x4 -- loaded as the accumulators' initial value, stored as one 16-B
 // write, its f16(x*g*2^-4) as one 8-B write (the four fp32 products, then one rounding each, as
 // gemm_resid_xg), and the four squares added into the lane's partial in column order
@@ -148,9 +153,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fg = lane >> 4;
-  // SWAP as gemm256_kernel's (the two tiles must give a prompt the same bits: prefill packing
-  // invariance): C^T, 4 consecutive columns of one row per lane
-  constexpr bool SWAP = true;
+  // the transposed accumulator as gemm256_kernel's (the two tiles must give a prompt the same
+  // bits: prefill packing invariance): C^T, 4 consecutive columns of one row per lane
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 4; ++n)
-          acc[m][n] = SWAP ? mfma16(bfr[n], af[m], acc[m][n]) : mfma16(af[m], bfr[n], acc[m][n]);
+          acc[m][n] = mfma16(bfr[n], af[m], acc[m][n]);
     }
     wait_vmcnt0();
     __syncthreads();
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     return;
   }
   gemm_rs_fold<GBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
-  if constexpr (SWAP) {
+  {
     // acc[m][n][j] = C[row 16m + fr][col 16n + 4fg + j] of the wave's 64x64
     float rv[4];
 #pragma unroll
@@ -283,46 +287,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
                 else ((float*)out)[o + j] = v[j];
               }
           }
-        }
-      }
-    }
-    return;
-  }
-  f32x4 rv4[4];  // the rows' norm factors, as gemm256_kernel's epilogue
-#pragma unroll
-  for (int m = 0; m < 4; ++m) rv4[m] = f32x4{1.f, 1.f, 1.f, 1.f};
-  if (rs.ssq) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) rv4[m] = *(const f32x4*)(rinv_s + wm * 64 + m * 16 + fg * 4);
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rv4[m][j] = rs_rinv(rv4[m][j], rs);
-  }
-#pragma unroll
-  for (int m = 0; m < 4; ++m) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = m0 + wm * 64 + m * 16 + fg * 4 + j;
-      if (row >= M) continue;
-      const float rv = rv4[m][j];
-      if constexpr (EPI == 2) {  // SwiGLU: n even = gate, n odd = up of the same 16 features
-#pragma unroll
-        for (int n = 0; n < 4; n += 2) {
-          const int col = n0 + wn * 64 + n * 16;  // multiple of 32
-          if (col >= N) continue;
-          const int f = (col >> 5) * 16 + fr;
-          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[m][n][j] * rv, acc[m][n + 1][j] * rv));
-        }
-      } else {
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int col = n0 + wn * 64 + n * 16 + fr;
-          if (col >= N) continue;
-          const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[m][n][j] * rv);
-          else if constexpr (EPI == 1) ((float*)out)[o] += acc[m][n][j];
-          else ((float*)out)[o] = acc[m][n][j] * rv;
         }
       }
     }
@@ -410,10 +374,9 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   const int wr = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fg = lane >> 4;
   const int sw = fr >> 1;  // swz2(row) for every fragment row (rows = 16-aligned base + fr)
-  // SWAP: the MFMA computes C^T (W fragment as the A operand), so a lane holds 4 CONSECUTIVE
-  // columns of one row -- the epilogues load / store 8 / 16 B per lane instead of one 2 / 4-B
-  // element (the swapped MFMA can round differently in the last bit: every GEMM tile swaps)
-  constexpr bool SWAP = true;
+  // the MFMA computes C^T (W fragment as the A operand), so a lane holds 4 CONSECUTIVE columns
+  // of one row -- the epilogues load / store 8 / 16 B per lane instead of one 2 / 4-B element
+  // (every GEMM tile does the same: the prefill packing invariance needs one set of bits)
   f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -452,8 +415,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2)
-          acc[qa * 4 + m][qb * 2 + n] = SWAP ? mfma16(bfr[n][s2], af[m][s2], acc[qa * 4 + m][qb * 2 + n])
-                                             : mfma16(af[m][s2], bfr[n][s2], acc[qa * 4 + m][qb * 2 + n]);
+          acc[qa * 4 + m][qb * 2 + n] = mfma16(bfr[n][s2], af[m][s2], acc[qa * 4 + m][qb * 2 + n]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
@@ -553,7 +515,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
     return;
   }
   gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
-  if constexpr (SWAP) {
+  {
     // acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x64: one row factor
     // per mi, the four columns of a (mi, ni) stored as one 8-B (fp16) / 16-B (fp32) write
     float rv[8];
@@ -608,53 +570,11 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
         }
       }
     }
-    return;
-  }
-  // the rows' norm factors: one ds_read_b128 per 4 rows, all issued ahead of the stores (a
-  // read + rsq per row inside the store loop was 32 serialised LDS round trips per lane,
-  // +2.7 % on the whole GEMM, profiles/r03/v11_gemm_rs_epilogue_ab.txt)
-  f32x4 rv4[8];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) rv4[mi] = f32x4{1.f, 1.f, 1.f, 1.f};
-  if (rs.ssq) {
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) rv4[mi] = *(const f32x4*)(rinv_s + wr * 128 + mi * 16 + fg * 4);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
-  }
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
-      if (row >= M) continue;
-      const float rv = rv4[mi][j];
-      if constexpr (EPI == 2) {  // SwiGLU: ni even = gate, ni odd = up of the same 16 features
-#pragma unroll
-        for (int ni = 0; ni < 4; ni += 2) {
-          const int col = n0 + wc * 64 + ni * 16;  // multiple of 32
-          if (col >= N) continue;
-          const int f = (col >> 5) * 16 + fr;
-          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
-        }
-      } else {
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int col = n0 + wc * 64 + ni * 16 + fr;
-          if (col >= N) continue;
-          const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[mi][ni][j] * rv);
-          else if constexpr (EPI == 1) ((float*)out)[o] += acc[mi][ni][j];
-          else ((float*)out)[o] = acc[mi][ni][j] * rv;
-        }
-      }
-    }
   }
 }
 
-// ---- 4-wave 256x256x64 variant (gemm variant 3, opt-in): 256 threads in 2 x 2, each wave a 128 x 128
+// ---- 4-wave 256x256x64 variant (gemm variant 3; the default dispatch's kernel for the stored epilogues,
+// variant 4): 256 threads in 2 x 2, each wave a 128 x 128
 // output (8 x 8 MFMA tiles, the 256 accumulators pinned in AGPRs, one wave per SIMD) -- the library
 // GEMM's geometry at this shape (hipBLASLt MT256x256x64_MI16x16 on 4 waves: 1455 vs 1215 TF/s on
 // the gate/up shape, same box, profiles/r05/v8_*).  Per K-tile a wave reads 32 KB of fragments for
@@ -729,13 +649,9 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
   // builtin, hipcc rotated one 4-register tile through a spare AGPR slot every MFMA (184
   // v_accvgpr_mov per K-tile); dependent MFMAs on one accumulator are interlocked, the reads after
   // the loop wait below
-  // SWAP (gemm256_kernel's): C^T, 4 consecutive columns of one row per lane
-  constexpr bool SWAP = true;
+  // the transposed accumulator (gemm256_kernel's): C^T, 4 consecutive columns of one row per lane
   auto mf1 = [&](int p, int i) {
-    if constexpr (SWAP)
-      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(bf[p][i & 7]), "v"(af[p][i >> 3]));
-    else
-      asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(af[p][i >> 3]), "v"(bf[p][i & 7]));
+    asm volatile("v_mfma_f32_16x16x32_f16 %0, %1, %2, %0" : "+a"(acc[i >> 3][i & 7]) : "v"(bf[p][i & 7]), "v"(af[p][i >> 3]));
   };
 
   const int nk = K / TBK;
@@ -831,7 +747,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
     return;
   }
   gemm_rs_fold<TBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
-  if constexpr (SWAP) {
+  {
     // acc[mi][ni][j] = C[row 16mi + fr][col 16ni + 4fg + j] of the wave's 128x128
     float rv[8];
 #pragma unroll
@@ -883,52 +799,13 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
         }
       }
     }
-    return;
-  }
-  f32x4 rv4[8];
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) rv4[mi] = f32x4{1.f, 1.f, 1.f, 1.f};
-  if (rs.ssq) {
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi) rv4[mi] = *(const f32x4*)(rinv_s + wr * 128 + mi * 16 + fg * 4);
-#pragma unroll
-    for (int mi = 0; mi < 8; ++mi)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) rv4[mi][j] = rs_rinv(rv4[mi][j], rs);
-  }
-#pragma unroll
-  for (int mi = 0; mi < 8; ++mi) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int row = m0 + wr * 128 + mi * 16 + fg * 4 + j;
-      if (row >= M) continue;
-      const float rv = rv4[mi][j];
-      if constexpr (EPI == 2) {
-#pragma unroll
-        for (int ni = 0; ni < 8; ni += 2) {
-          const int col = n0 + wc * 128 + ni * 16;
-          if (col >= N) continue;
-          const int f = (col >> 5) * 16 + fr;
-          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(silu_mul(acc[mi][ni][j] * rv, acc[mi][ni + 1][j] * rv));
-        }
-      } else {
-#pragma unroll
-        for (int ni = 0; ni < 8; ++ni) {
-          const int col = n0 + wc * 128 + ni * 16 + fr;
-          if (col >= N) continue;
-          const size_t o = (size_t)row * ldo + col;
-          if constexpr (EPI == 0) ((f16_t*)out)[o] = f2h(acc[mi][ni][j] * rv);
-          else ((float*)out)[o] = acc[mi][ni][j] * rv;
-        }
-      }
-    }
   }
 }
 
 // 0: heuristic (8-wave big tile), 1: 128x128, 2: 256x256 8-wave, 3: 256x256 4-wave, 4 (default):
 // the heuristic with the 4-wave kernel for the stored epilogues and the 8-wave one for the residual
 // epilogue (the 4-wave residual form spills) -- QKV 437 -> 422 us, gate/up 1327 -> 1321 us per
-// launch, prefill 87.0 -> 86.2 ms per configs[1] step (profiles/r05/v11_*).  Tests and sweeps set
+// launch, prefill 87.0 -> 86.2 ms per configs[1] step (profiles/r05/v11_ab3_*, v11_prof_*).  Tests and sweeps set
 // it (ms_set_gemm_variant, MS_GEMM_VARIANT); every variant gives the same bits
 static int g_gemm_variant = [] { const char* e = getenv("MS_GEMM_VARIANT"); return e ? atoi(e) : 4; }();
 

@@ -118,7 +118,8 @@ int gemm_resid_tiles(int M, int N);
 bool gemm_rs_tiles_ok(int M, int N, int tiles);
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo,
                  int epi, hipStream_t s, const RowScale* rs = nullptr, const GemmResid* gr = nullptr);
-// tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256
+// tile choice: 0 = heuristic (256x256 8-phase for M, N >= 1024), 1 = 128x128, 2 = 256x256,
+// 3 = 256x256 on 4 waves, 4 (default) = the heuristic with 3 for the stored epilogues
 void set_gemm_variant(int v);
 // the Q6_K lm_head argmax GEMV: grid-stride two-stage loop (default) or one-tile blocks
 void set_qgemv_gs(bool on);
@@ -286,7 +287,7 @@ void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int
 bool qkv_attn_supported(int B, int max_batch, int H, int Hq, int Hk, int max_len, int ppb, int split_qkv);
 // diagnostic: the latest launch's phase stamps [256][16] (MS_QA_STAMPS=1), 100 MHz ticks
 void qkv_attn_stamps(unsigned long long* host, int n);
-// decode attention v2's per-block phase stamps of its latest launch (MS_A2_STAMPS=1), [1024][24]
+// decode attention v2's per-block phase stamps of its latest launch (MS_A2_STAMPS=1), [1024][32]
 void attn2_stamps(unsigned long long* host, int n);
 void launch_qkv_attn(const f16_t* xb, const f16_t* wqkv, float* qkv32, const DecodeQKV& qa, f16_t* out, int Hq,
                      int Hk, KVView kv, DecodeAttnArgs a, float* ws, int ppb, unsigned* sync, unsigned* err,

@@ -29,7 +29,7 @@ ap.add_argument("--prompt", type=int, default=2048)
 args = ap.parse_args()
 import bench  # noqa: E402
 
-NB, NS = 1024, 24
+NB, NS = 1024, 32
 cfg = LLAMA32_3B.with_(n_layers=2)
 chunks = bench.synthetic_chunks(8, args.prompt, doc=0, vocab=cfg.vocab, bos=cfg.bos_id)
 with Engine(cfg, device=0, max_batch=8, max_ctx=args.prompt + 256, max_prefill_tokens=8 * args.prompt) as e:
@@ -60,6 +60,11 @@ print(f"decode attention v2, latest launch ({len(ts)} blocks), {args.prompt}-tok
       f"us since the first block entry")
 print(f"{'phase':34s} {'min':>7s} {'median':>7s} {'p90':>7s} {'max':>7s}  n")
 row("block entry", ts[:, 0])
+row("last wave entry", ts[:, 24])
+row("wave 0 prologue loads issued", ts[:, 26])
+row("last wave prologue loads issued", ts[:, 25])
+row("wave 0 prologue loads landed", ts[:, 22])
+row("last wave prologue loads landed", ts[:, 23])
 row("prologue done (wave 0)", ts[:, 2])
 sd = ts[:, 3:12]
 pv = ts[:, 12:21]
