@@ -23,7 +23,7 @@ FLOP_PER_BUSY_CYCLE = 1024
 
 def main():
     path, out = sys.argv[1], sys.argv[2]
-    subs = sys.argv[3:] or ["gemm256_kernel", "gemm_kernel", "attn_prefill_kernel"]
+    subs = sys.argv[3:] or ["gemm256_kernel", "gemm4w_kernel", "gemm_kernel", "attn_prefill_kernel"]
     val = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for r in csv.DictReader(open(path)):
