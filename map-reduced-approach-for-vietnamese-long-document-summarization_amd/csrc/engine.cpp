@@ -1832,6 +1832,9 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
     REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
     REQUIRE(epi != MS_EPI_ADD_F32 || (N % 4 == 0 && ldo % 4 == 0), MS_EINVAL,
             "residual gemm: N and ldo multiples of 4 (16-B x rows)");
+    // the epilogues store 4 consecutive columns per lane (8 B fp16, 16 B fp32)
+    REQUIRE(((uintptr_t)out & ((epi == MS_EPI_ADD_F32 || epi == MS_EPI_STORE_F32) ? 15 : 7)) == 0, MS_EINVAL,
+            "gemm: out must be 16-B (fp32) / 8-B (fp16) aligned");
     REQUIRE(!g_op_rs.ssq || gemm_rs_tiles_ok(M, N, g_op_rs.tiles), MS_EINVAL,
             "gemm row scale: at most 24 tiles of statistics (kGemmRsTiles, both GEMM tiles)");
     launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
@@ -1844,7 +1847,8 @@ int ms_op_gemm_resid(const void* A, const void* W, float* x, void* xg_out, const
     REQUIRE(A && W && x && xg_out && gamma && ssq_out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL,
             "bad gemm_resid operands (K % 64 == 0)");
     REQUIRE(gemm_resid_tiles(M, N) <= kGemmRsTiles, MS_EINVAL, "gemm_resid: N over 24 column tiles");
-    REQUIRE(N % 4 == 0, MS_EINVAL, "gemm_resid: N a multiple of 4 (16-B x rows)");
+    REQUIRE(N % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)xg_out & 7) == 0, MS_EINVAL,
+            "gemm_resid: N a multiple of 4, x 16-B and xg 8-B aligned (vector rows)");
     GemmResid gr{(const f16_t*)gamma, (f16_t*)xg_out, ssq_out};
     launch_gemm((const f16_t*)A, (const f16_t*)W, x, M, N, K, N, MS_EPI_ADD_F32, (hipStream_t)stream, nullptr, &gr);
   });
