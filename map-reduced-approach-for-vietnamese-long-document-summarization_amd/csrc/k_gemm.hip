@@ -78,14 +78,15 @@ __device__ __forceinline__ void gemm_rs_fold(const RowScale& rs, float* rinv_s, 
 // x[row][c0 .. c0+3] as one f32x4 -- loaded as the accumulators' initial value, stored as one 16-B
 // write, its f16(x*g*2^-4) as one 8-B write (the four fp32 products, then one rounding each, as
 // gemm_resid_xg), and the four squares added into the lane's partial in column order
-__device__ __forceinline__ void gemm_resid_x4(const GemmResid& gr, float* x, size_t o, f32x4 v, const f16_t (&g)[4],
-                                              bool fuse, float& ss) {
+__device__ __forceinline__ void gemm_resid_x4(const GemmResid& gr, float* x, size_t o, f32x4 v, uint2 g, bool fuse,
+                                              float& ss) {
   *(f32x4*)(x + o) = v;
   if (!fuse) return;
+  const float gf[4] = {h_lo(g.x), h_hi(g.x), h_lo(g.y), h_hi(g.y)};  // the 4 gains, packed fp16
   float p[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    p[j] = v[j] * h2f(g[j]) * kXgScale;
+    p[j] = v[j] * gf[j] * kXgScale;
     asm volatile("" : "+v"(p[j]));
   }
   *(uint2*)(gr.xg + o) = uint2{pack2h(p[0], p[1]), pack2h(p[2], p[3])};
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
   // load here made the compiler drain vmcnt inside the K loop); read at the epilogue
   gemm_rs_dma<GBM, 4>(rs, M, m0, rinv_s, rs_stage);
   // residual epilogue: x as the accumulators' initial value (as gemm256_kernel)
-  f16_t g4[4][4] = {};  // raw bits, converted in the epilogue
+  uint2 g4[4] = {};  // the gains as packed fp16 bits, converted in the epilogue
   if constexpr (EPI == 1) {
     // transposed: acc[m][n] = x[row 16m + fr][cols 16n + 4fg .. +3], one 16-B load each
 #pragma unroll
@@ -180,9 +181,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;  // unconditional load (no merge wait)
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
-      const uint2 w = *(const uint2*)(gp + min(n0 + wn * 64 + n * 16 + 4 * fg, N - 4));
-      g4[n][0] = (f16_t)(w.x & 0xFFFF); g4[n][1] = (f16_t)(w.x >> 16);
-      g4[n][2] = (f16_t)(w.y & 0xFFFF); g4[n][3] = (f16_t)(w.y >> 16);
+      g4[n] = *(const uint2*)(gp + min(n0 + wn * 64 + n * 16 + 4 * fg, N - 4));
     }
   }
   stage(0, 0);
@@ -427,7 +426,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
   // residual epilogue: the tile's x is the accumulators' initial value, loaded ahead of the
   // first K tile (the prologue's vmcnt waits retire it with tile 0), so the MFMAs add A . W^T
   // onto x and the epilogue only stores -- no load round trips after the K loop
-  f16_t g4[4][4] = {};  // raw bits: converted in the epilogue (a conversion here waited)
+  uint2 g4[4] = {};  // the gains as packed fp16 bits: converted in the epilogue (a conversion here waited)
   if constexpr (EPI == 1) {
     // transposed: acc[mi][ni] = x[row 16mi + fr][cols 16ni + 4fg .. +3], one 16-B load each
 #pragma unroll
@@ -442,9 +441,7 @@ __global__ __launch_bounds__(512, 1) void gemm256_kernel(const f16_t* __restrict
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
-      const uint2 w = *(const uint2*)(gp + min(n0 + wc * 64 + ni * 16 + 4 * fg, N - 4));
-      g4[ni][0] = (f16_t)(w.x & 0xFFFF); g4[ni][1] = (f16_t)(w.x >> 16);
-      g4[ni][2] = (f16_t)(w.y & 0xFFFF); g4[ni][3] = (f16_t)(w.y >> 16);
+      g4[ni] = *(const uint2*)(gp + min(n0 + wc * 64 + ni * 16 + 4 * fg, N - 4));
     }
   }
   // prologue: tile 0 whole, then UAt/UBr of tile 1; tile 0 landed when <= 4 loads remain
@@ -656,7 +653,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
 
   const int nk = K / TBK;
   gemm_rs_dma<TBM, 4>(rs, M, m0, rinv_s, rs_stage);
-  f16_t g8[8][4] = {};
+  uint2 g8[8] = {};
   if constexpr (EPI == 1) {
 #pragma unroll
     for (int mi = 0; mi < 8; ++mi)
@@ -669,9 +666,7 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const f16_t* __restrict_
     const f16_t* gp = gr.xg ? gr.gamma : (const f16_t*)A;
 #pragma unroll
     for (int ni = 0; ni < 8; ++ni) {
-      const uint2 w = *(const uint2*)(gp + min(n0 + wc * 128 + ni * 16 + 4 * fg, N - 4));
-      g8[ni][0] = (f16_t)(w.x & 0xFFFF); g8[ni][1] = (f16_t)(w.x >> 16);
-      g8[ni][2] = (f16_t)(w.y & 0xFFFF); g8[ni][3] = (f16_t)(w.y >> 16);
+      g8[ni] = *(const uint2*)(gp + min(n0 + wc * 128 + ni * 16 + 4 * fg, N - 4));
     }
   }
   // prologue: tiles 0 and 1 in flight, tile 0 landed everywhere, its k-step-0 fragments read
@@ -815,6 +810,9 @@ static bool gemm_big(int M, int N) {
   return g_gemm_variant == 2 || g_gemm_variant == 3 ||
          ((g_gemm_variant == 0 || g_gemm_variant == 4) && M >= 1024 && N >= 1024);
 }
+// the 4-wave tile for this launch: variant 3 always, 4 for the stored epilogues (the residual
+// O at K = 3072 on it measured 333 vs 321 us in the engine, r05/v18_*)
+static bool gemm_4wave(int epi) { return g_gemm_variant == 3 || (g_gemm_variant == 4 && epi != 1); }
 
 int gemm_resid_tiles(int M, int N) {
   (void)M;
@@ -833,7 +831,7 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
   GemmResid gr{};
   if (gr_in && epi == 1) gr = *gr_in;
 #define GL(KERN, EPI_, BLK) MS_LAUNCH(KERN<EPI_>, dim3(grid), dim3(BLK), 0, s, A, W, out, M, N, K, ldo, rs, gr)
-  if (big && (g_gemm_variant == 3 || (g_gemm_variant == 4 && epi != 1)) && K % TBK == 0) {
+  if (big && gemm_4wave(epi) && K % TBK == 0) {
     const int grid = ((M + TBM - 1) / TBM) * ((N + TBN - 1) / TBN);
     switch (epi) {
       case 0: GL(gemm4w_kernel, 0, 256); break;
