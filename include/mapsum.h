@@ -240,6 +240,10 @@ int ms_set_gemm_variant(int32_t variant);
    argmax, the Q4_K gate/up SwiGLU) take it (1, the default) or run one-tile blocks (0); the
    two give bit-identical outputs */
 int ms_set_qgemv_gs(int32_t on);
+/* tuning/test hook: decode attention's split combine on the XCD-matched grid (1, default) or the
+   (B, Hq) grid (0), and the v2 prologue form (0 default, 3 a dedicated prologue wave); every
+   setting gives the same bits.  Engines capture their decode graphs with the current setting. */
+int ms_set_attn_tuning(int32_t combine_grp, int32_t order);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,

@@ -1862,6 +1862,12 @@ int ms_set_gemm_variant(int32_t v) {
   return MS_OK;
 }
 
+int ms_set_attn_tuning(int32_t combine_grp, int32_t order) {
+  if (combine_grp < 0 || combine_grp > 1 || (order != 0 && order != 3)) return MS_EINVAL;
+  set_attn_tuning(combine_grp, order);
+  return MS_OK;
+}
+
 int ms_set_qgemv_gs(int32_t on) {
   if (on < 0 || on > 1) return MS_EINVAL;
   set_qgemv_gs(on != 0);

@@ -675,11 +675,16 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
   out[(size_t)b * Hq * kHeadDim + hq * kHeadDim + d] = f2h(O / L);
 }
 
-// MS_COMBINE_GRP=0: the (B, Hq) grid for v2 too (placement only: the same bits either way)
-static bool combine_grp_ok(int B, int Hk) {
-  static const bool on = [] { const char* e = getenv("MS_COMBINE_GRP"); return !(e && atoi(e) == 0); }();
-  return on && (B * Hk) % 8 == 0;
+// decode-attention tuning (MS_COMBINE_GRP / MS_A2_ORDER, or ms_set_attn_tuning): the combine's
+// XCD-matched grid (placement only) and the v2 prologue form (3: the prologue wave); both give
+// the same bits.  Read at launch: a captured decode graph keeps what it was captured with.
+static int g_combine_grp = [] { const char* e = getenv("MS_COMBINE_GRP"); return e ? atoi(e) : 1; }();
+static int g_a2_order = [] { const char* e = getenv("MS_A2_ORDER"); return e ? atoi(e) : 0; }();
+void set_attn_tuning(int combine_grp, int order) {
+  g_combine_grp = combine_grp;
+  g_a2_order = order;
 }
+static bool combine_grp_ok(int B, int Hk) { return g_combine_grp != 0 && (B * Hk) % 8 == 0; }
 
 // the combine launch: (B, Hq) grid, or with grp the 1-D XCD-matched grid of the v2 kernel
 static void launch_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int nsplit, bool grp,
@@ -1213,11 +1218,10 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
   const dim3 grid(a.B * Hk * nsplit);
   const size_t lds = attn2_lds_bytes(ppb, Hq / Hk);
-  // MS_A2_ORDER=3: the prologue-wave form (PW; opt-in -- bit-identical, measured no faster: the
-  // first S moves from 12.7 to 8.7 us into the block, but the block still ends when its last
-  // page lands, 18.84 vs 18.72 us per launch, decode 2.109 vs 2.105 ms per step, profiles/r05/v12_*)
-  static const int order = [] { const char* e = getenv("MS_A2_ORDER"); return e ? atoi(e) : 0; }();
-  const bool pw = order == 3 && qa.slabs && !cnt && attn2_pw_ok(Hq / Hk);
+  // order 3: the prologue-wave form (PW; opt-in -- bit-identical, measured no faster: the first
+  // S moves from 12.7 to 8.7 us into the block, but the block still ends when its last page
+  // lands, 18.84 vs 18.72 us per launch, decode 2.109 vs 2.105 ms per step, profiles/r05/v12_*)
+  const bool pw = g_a2_order == 3 && qa.slabs && !cnt && attn2_pw_ok(Hq / Hk);
   static unsigned long long* stamps = [] {
     const char* e = getenv("MS_A2_STAMPS");
     void* p = nullptr;

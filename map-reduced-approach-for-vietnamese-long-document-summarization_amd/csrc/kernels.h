@@ -123,6 +123,9 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
 void set_gemm_variant(int v);
 // the Q6_K lm_head argmax GEMV: grid-stride two-stage loop (default) or one-tile blocks
 void set_qgemv_gs(bool on);
+// decode attention: the combine's XCD-matched grid (1, default) and the v2 prologue form
+// (0 default, 3 the prologue wave) -- placement / schedule only, the same bits
+void set_attn_tuning(int combine_grp, int order);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {

@@ -558,6 +558,28 @@ def test_decode_tail_bit_exact(dev, chunks, monkeypatch, slots):
     assert outs[0] == outs[1]
 
 
+def test_decode_attention_tuning_bit_exact(dev, chunks):
+    """Decode attention's tuning knobs are placement / schedule only (ms_set_attn_tuning): the
+    split combine on the XCD-matched 1-D grid (default) or the (B, Hq) grid, and the v2 kernel
+    with a dedicated prologue wave (order 3, opt-in) -- identical greedy ids over chained runs."""
+    lib = L.load()
+    outs = {}
+    try:
+        for grp, order in ((1, 0), (0, 0), (1, 3)):
+            L.check(lib.ms_set_attn_tuning(grp, order))
+            e = Engine(CFG, device=0, max_batch=NCHUNK, max_ctx=P + 64, max_prefill_tokens=NCHUNK * P)
+            try:
+                e.init_synthetic(SEED, STD, JIT)
+                res = e.generate(list(chunks), num_predict=40, ignore_eos=True)
+                outs[(grp, order)] = [r.ids for r in res]
+            finally:
+                e.close()
+    finally:
+        L.check(lib.ms_set_attn_tuning(1, 0))
+    assert outs[(0, 0)] == outs[(1, 0)]
+    assert outs[(1, 3)] == outs[(1, 0)]
+
+
 def test_prefill_packing_invariance(dev):
     """A prompt's prefill does not depend on what it is packed with: alone (600 rows: the
     128x128 GEMM tile) and behind a 1500-token prompt (2100 rows: the 256x256 tile) its hidden
