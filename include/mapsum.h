@@ -244,6 +244,12 @@ int ms_set_qgemv_gs(int32_t on);
    (B, Hq) grid (0), and the v2 prologue form (0 default, 3 a dedicated prologue wave); every
    setting gives the same bits.  Engines capture their decode graphs with the current setting. */
 int ms_set_attn_tuning(int32_t combine_grp, int32_t order);
+/* tuning/test hook: the large-batch decode skinny GEMM on 4-wave blocks (1) or on 8-wave
+   blocks that split each 128-k step in two k halves (2, the default); the two sum in
+   different orders, each independent of the batch rows.  Engines of <= 128 slots take the
+   setting for their gate/up launch at creation (set it before ms_engine_create);
+   ms_op_dgemm takes it where it applies (M <= 128, K % (128 S) == 0). */
+int ms_set_dgemm_kh(int32_t kh);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,

@@ -140,6 +140,11 @@ struct ms_engine {
   // at M = 16 the GEMV and the skinny GEMM tie over a layer's four projections, at M = 32
   // the skinny GEMM takes 30 % less (profiles/r02/v7_dgemm_lds_sync_ab.txt).
   int dgemm_min = 24, dsplit_qkv = 6, dsplit_o = 4, dsplit_down = 8;
+  // gate/up skinny-GEMM block form (k_dgemm.hip kh), fixed per engine like the regime: the
+  // library setting (2, the default: k split over the two wave groups of an 8-wave block;
+  // 41.4 -> 34.9 us at M = 128, profiles/r05/v20_*) for engines of <= 128 slots; the split
+  // projections and the lm_head keep the 4-wave block (as fast or faster there)
+  int dgemm_kh = 1;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
   // decode attention with one page per wave (k_attn.hip v2, MS_ATTN_V2), attn_ppb waves / pages
@@ -388,10 +393,10 @@ struct ms_engine {
   bool fused_decode(int B) const {
     if (large(B))
       return B <= kMaxSlabRows && attn_slabs && residual_rmsnorm_supported(kMaxSplit, H) &&
-             dgemm_supported(B, QKVN, H, dsplit_qkv, MS_GEMV_EPI_STORE_F32) &&
-             dgemm_supported(B, H, Hq * D, dsplit_o, MS_GEMV_EPI_STORE_F32) &&
-             dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32) &&
-             dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU) && (2 * F) % 32 == 0 &&
+             dgemm_supported(B, QKVN, H, dsplit_qkv, MS_GEMV_EPI_STORE_F32, 1) &&
+             dgemm_supported(B, H, Hq * D, dsplit_o, MS_GEMV_EPI_STORE_F32, 1) &&
+             dgemm_supported(B, H, F, dsplit_down, MS_GEMV_EPI_STORE_F32, 1) &&
+             dgemm_supported(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU, dgemm_kh) && (2 * F) % 32 == 0 &&
              attn_decode_supported(B, Hq, Hk, max_pages * kPage);
     // row groups (K-quant engines above 64 rows): split-K slabs and SwiGLU only, no residual
     // epilogue (resid_fused is off in large engines), one residual_rmsnorm over all rows
@@ -443,7 +448,7 @@ struct ms_engine {
     ga.slab_rows = slab_rows;
     int used = 1;
     if (large(M)) {  // skinny GEMM on the fp16 weights (K-quant copies included)
-      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
+      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1);
       used = Sl;
     } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
       // Q4_K/Q6_K: same split-K as fp16 (a 16-row tile carries 3.6x fewer weight bytes, so
@@ -553,7 +558,7 @@ struct ms_engine {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
       prof_begin(K_GEMV);
-      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn);
+      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn, dgemm_kh);
       prof_end(K_GEMV);
     } else {
       GemvArgs gg{};
@@ -865,6 +870,11 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
+    E.dgemm_kh = cfg->max_batch <= 128 ? dgemm_kh_setting() : 1;
+    if (const char* v = getenv("MS_DSPLIT_QKV")) E.dsplit_qkv = atoi(v);
+    if (const char* v = getenv("MS_DSPLIT_O")) E.dsplit_o = atoi(v);
+    if (const char* v = getenv("MS_DSPLIT_DOWN")) E.dsplit_down = atoi(v);
+    for (int* d : {&E.dsplit_qkv, &E.dsplit_o, &E.dsplit_down}) *d = std::min(std::max(*d, 1), (int)ms_engine::kMaxSplit);
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
@@ -1447,11 +1457,12 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   // every layer leaves xb = f16(x * the next gain) with its deferred scale in cur_rs
   for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
   const RowScale rs = E.cur_rs;
-  if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX)) {
+  if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX, 1)) {
     const int tiles = E.V / 16;
     E.prof_begin(K_LMHEAD);
     // no row scale: r > 0 keeps every row's order (the logits themselves are never stored)
-    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream);
+    // 4-wave blocks always: a 2004-block grid keeps two per CU (k_dgemm.hip kh)
+    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1);
     E.prof_end(K_LMHEAD);
     decode_tail(E, B, d, tiles);
     return;
@@ -1865,6 +1876,12 @@ int ms_set_gemm_variant(int32_t v) {
 int ms_set_attn_tuning(int32_t combine_grp, int32_t order) {
   if (combine_grp < 0 || combine_grp > 1 || (order != 0 && order != 3)) return MS_EINVAL;
   set_attn_tuning(combine_grp, order);
+  return MS_OK;
+}
+
+int ms_set_dgemm_kh(int32_t kh) {
+  if (kh != 1 && kh != 2) return MS_EINVAL;
+  set_dgemm_kh(kh);
   return MS_OK;
 }
 

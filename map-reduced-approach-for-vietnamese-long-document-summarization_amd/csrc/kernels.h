@@ -126,6 +126,9 @@ void set_qgemv_gs(bool on);
 // decode attention: the combine's XCD-matched grid (1, default) and the v2 prologue form
 // (0 default, 3 the prologue wave) -- placement / schedule only, the same bits
 void set_attn_tuning(int combine_grp, int order);
+// large-batch skinny GEMM: 1 = 4-wave blocks, 2 = 8-wave blocks with the K step split in halves
+// (S = 1 launches; a different but M-independent sum order)
+void set_dgemm_kh(int kh);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {
@@ -207,9 +210,13 @@ void launch_gemv_ex(const f16_t* X, const f16_t* W, void* out, int M, int N, int
 // large-batch decode projections (k_dgemm.hip): 64 weight rows x all M <= 256 rows per block,
 // X shared through LDS; S > 1 = split-K fp32 slabs [S][M][N] (STORE_F32 only).  Epilogues as
 // the GEMV's except ROPE_KV; N % 64 == 0, K % (64 S) == 0.
-bool dgemm_supported(int M, int N, int K, int S, int epi);
+// kh: 1 = 4-wave blocks, 2 = 8-wave blocks splitting each 128-k step in two k halves (then
+// K % (128 S) == 0 and M <= 128), 0 = the library setting (set_dgemm_kh) where it applies
+// (M <= 128, K % (128 S) == 0), else 1
+bool dgemm_supported(int M, int N, int K, int S, int epi, int kh = 0);
 void launch_dgemm(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  hipStream_t s, const RowScale* rs = nullptr);
+                  hipStream_t s, const RowScale* rs = nullptr, int kh = 0);
+int dgemm_kh_setting();
 
 // ---- ggml K-quant weights (k_qgemv.hip)
 enum { MS_QT_Q4_K = 12, MS_QT_Q6_K = 14 };  // ggml_type ids

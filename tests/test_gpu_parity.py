@@ -145,14 +145,22 @@ def test_gemv_vs_torch(lib, dev, M, N, K, epi):
             assert torch.equal(first, o), "gemv must be deterministic"
 
 
+@pytest.fixture(params=[1, 2], ids=["kh1", "kh2"])
+def dgemm_kh(lib, request):
+    """The skinny GEMM's block form (ms_set_dgemm_kh), restored to the default afterwards."""
+    L.check(lib.ms_set_dgemm_kh(request.param))
+    yield request.param
+    L.check(lib.ms_set_dgemm_kh(2))
+
+
 @pytest.mark.parametrize("M", [1, 17, 64, 100, 256])
 @pytest.mark.parametrize("N,K,S,epi", [(1024, 768, 1, L.MS_EPI_STORE_F16), (768, 2048, 1, L.MS_EPI_ADD_F32),
                                        (2048, 768, 1, L.MS_EPI_SWIGLU), (3072, 8192, 4, L.MS_EPI_STORE_F32),
                                        (5120, 3072, 6, L.MS_EPI_STORE_F32), (4096, 768, 1, L.MS_EPI_ARGMAX)])
-def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
-    """The large-batch decode GEMM (k_dgemm.hip) against a float64 reference: fp32 outputs
-    differ only by summation order; split-K slabs are the exact partial products; the
-    argmax partials merge to the fp32 logits' argmax."""
+def test_dgemm_vs_fp64(lib, dev, dgemm_kh, M, N, K, S, epi):
+    """The large-batch decode GEMM (k_dgemm.hip, both block forms) against a float64 reference:
+    fp32 outputs differ only by summation order; split-K slabs are the exact partial products;
+    the argmax partials merge to the fp32 logits' argmax."""
     g = torch.Generator(device="cpu").manual_seed(M * 7 + N + K + S + epi)
     X = _f16(torch.randn(M, K, generator=g)).to(dev)
     W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
@@ -191,6 +199,27 @@ def test_dgemm_vs_fp64(lib, dev, M, N, K, S, epi):
     L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), out.data_ptr(), M, N, K, S, ldo, epi, _stream()))
     torch.cuda.synchronize()
     assert rel(out.double().cpu(), exp) < tol
+
+
+@pytest.mark.parametrize("N,K,S,epi", [(16384, 3072, 1, L.MS_EPI_SWIGLU), (3072, 8192, 4, L.MS_EPI_STORE_F32),
+                                       (2048, 3072, 1, L.MS_EPI_STORE_F16)])
+def test_dgemm_rows_independent_of_batch(lib, dev, dgemm_kh, N, K, S, epi):
+    """A row's skinny-GEMM result is bitwise the same whatever the other rows of the launch
+    (the engine's batch-invariance contract), for both block forms -- 24..128 rows, the sizes
+    a <= 128-slot engine runs (engine gate/up at full width, N = 16384)."""
+    g = torch.Generator(device="cpu").manual_seed(N + K + S + epi)
+    X = _f16(torch.randn(128, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    ncol = N // 2 if epi == L.MS_EPI_SWIGLU else N
+    dt = torch.float32 if epi == L.MS_EPI_STORE_F32 else torch.float16
+    outs = {}
+    for M in (24, 77, 128):
+        o = torch.zeros(S, M, ncol, dtype=dt, device=dev)
+        L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), o.data_ptr(), M, N, K, S, ncol, epi, _stream()))
+        torch.cuda.synchronize()
+        outs[M] = o.cpu()
+    for M in (77, 128):
+        assert torch.equal(outs[M][:, :24], outs[24]), M
 
 
 @pytest.mark.parametrize("M", [1, 8, 16])

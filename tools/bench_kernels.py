@@ -112,7 +112,7 @@ def bench_dgemm(lib):
                                     ("lm_head", 128256, 3072, 5, (1,))]:
         Ws = [torch.randn(N, K, device=dev).to(torch.float16) * 0.02
               for _ in range(max(2, -(-512 * 2**20 // (N * K * 2))))]
-        for M in (8, 16, 32, 64, 128, 256):
+        for M in (32, 64, 128, 256):
             X = torch.randn(M, K, device=dev).to(torch.float16)
             out = torch.zeros(8 * M * N, device=dev)
             wbytes = N * K * 2
@@ -314,6 +314,7 @@ if __name__ == "__main__":
     ap.add_argument("--torch", action="store_true", help="gemm: also time torch.matmul (hipBLASLt) on the same operands")
     ap.add_argument("--ref-lib", default="", help="gemm: a second build (e.g. libmapsum_base.so) timed and compared")
     ap.add_argument("--resid", action="store_true", help="gemm: O / down through ms_op_gemm_resid (the engine's form)")
+    ap.add_argument("--kh", type=int, default=1, help="dgemm: block form (ms_set_dgemm_kh: 1 4-wave, 2 k-half 8-wave)")
     a = ap.parse_args()
     lib = L.load()
     if a.what == "gemv":
@@ -323,6 +324,7 @@ if __name__ == "__main__":
     elif a.what == "split":
         bench_split(lib, a.m)
     elif a.what == "dgemm":
+        assert lib.ms_set_dgemm_kh(a.kh) == 0
         bench_dgemm(lib)
     elif a.what == "qgemv":
         bench_qgemv(lib, a.m)
