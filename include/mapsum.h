@@ -250,6 +250,10 @@ int ms_set_attn_tuning(int32_t combine_grp, int32_t order);
    setting for their gate/up launch at creation (set it before ms_engine_create);
    ms_op_dgemm takes it where it applies (M <= 128, K % (128 S) == 0). */
 int ms_set_dgemm_kh(int32_t kh);
+/* tuning/test hook: ms_op_dgemm's weight rows per block, 64 (4 row groups, the default) or 128
+   (8; 4-wave-group blocks only, M <= 128, N % 128 == 0, else 64) -- the same bits either way.
+   Engines choose per projection (128 for QKV, down and the lm_head at <= 128 rows). */
+int ms_set_dgemm_wn(int32_t wn);
 /* decode skinny GEMM (M <= 64): same contract; workspace >= ms_op_gemv_workspace() bytes */
 int64_t ms_op_gemv_workspace(int32_t M, int32_t N, int32_t K);
 int ms_op_gemv(const void* X, const void* W, void* out, int32_t M, int32_t N, int32_t K,

@@ -145,6 +145,10 @@ struct ms_engine {
   // 41.4 -> 34.9 us at M = 128, profiles/r05/v20_*) for engines of <= 128 slots; the split
   // projections and the lm_head keep the 4-wave block (as fast or faster there)
   int dgemm_kh = 1;
+  // weight-row groups per skinny-GEMM block (k_dgemm.hip wn) for launches of <= 128 rows: the
+  // 128-row block for QKV, down and the lm_head (down 22.3 -> 20.4 us, lm_head 262 -> 241 us at
+  // M = 128, profiles/r05/v21_*), 64 rows for O (15.6 vs 12.9 us at its split 4); bit-identical
+  int dwn_qkv = 8, dwn_o = 4, dwn_down = 8, dwn_lm = 8;
   bool large_engine = false;
   int attn_ppw = 2;  // decode attention pages per wave, fixed per engine (k_attn.hip)
   // decode attention with one page per wave (k_attn.hip v2, MS_ATTN_V2), attn_ppb waves / pages
@@ -424,31 +428,34 @@ struct ms_engine {
 
   // normalised projection into fp32 partial slabs [S][M][N], rows scaled by cur_rs; returns
   // the number of slabs written
+  // dwn: the skinny GEMM's weight-row groups per block (k_dgemm.hip wn; 8 = 128-row blocks,
+  // the same bits as 4) for launches of <= 128 rows
   int proj_split(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
-                 const RowScale* rs) {
+                 const RowScale* rs, int dwn = 4) {
     if (row_groups(M)) {
       // every group must write the same number of slabs: the fold adds S slabs for all rows
       int used = 0;
       for (int r0 = 0; r0 < M; r0 += kMaxGemvRows) {
         const RowScale g = rs ? rs_rows(*rs, r0) : RowScale{};
         const int u = proj_split_rows(q, X + (size_t)r0 * K, W, std::min(M - r0, (int)kMaxGemvRows), N, K, S, Sl,
-                                      rs ? &g : nullptr, slabs + (size_t)r0 * N, M);
+                                      rs ? &g : nullptr, slabs + (size_t)r0 * N, M, dwn);
         REQUIRE(used == 0 || u == used, MS_EIO, "row groups split a projection differently");
         used = u;
       }
       return used;
     }
-    return proj_split_rows(q, X, W, M, N, K, S, Sl, rs, slabs, 0);
+    return proj_split_rows(q, X, W, M, N, K, S, Sl, rs, slabs, 0, dwn);
   }
   int proj_split_rows(const QSlot* q, const f16_t* X, const f16_t* W, int M, int N, int K, int S, int Sl,
-                      const RowScale* rs, float* slabs, int slab_rows) {
+                      const RowScale* rs, float* slabs, int slab_rows, int dwn) {
     prof_begin(K_GEMV);
     GemvArgs ga{};
     if (rs) ga.rs = *rs;
     ga.slab_rows = slab_rows;
     int used = 1;
     if (large(M)) {  // skinny GEMM on the fp16 weights (K-quant copies included)
-      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1);
+      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1,
+                   M <= 128 && N % 128 == 0 ? dwn : 4);
       used = Sl;
     } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
       // Q4_K/Q6_K: same split-K as fp16 (a 16-row tile carries 3.6x fewer weight bytes, so
@@ -482,7 +489,7 @@ struct ms_engine {
   // projection (gain g_next) -- in the GEMV epilogue (resid_fused: RESID_SSQ on resid_rt-row
   // tiles, 256 tiles of statistics) or as split-K slabs + one residual_rmsnorm launch
   void resid_update(const QSlot* q, const f16_t* X, const f16_t* W, int B, int K, int S, int Sl,
-                    const f16_t* g_next) {
+                    const f16_t* g_next, int dwn) {
     if (resid_fused(q)) {
       GemvArgs ga{};
       ga.rt = resid_rt;
@@ -498,7 +505,7 @@ struct ms_engine {
       pending_split = 0;
       cur_rs = make_row_scale(ssq, H / resid_rt, H, cfg.norm_eps);
     } else {
-      pending_split = proj_split(q, X, W, B, H, K, S, Sl, nullptr);
+      pending_split = proj_split(q, X, W, B, H, K, S, Sl, nullptr, dwn);
       residual_norm(g_next, B);
     }
   }
@@ -523,7 +530,7 @@ struct ms_engine {
       // QKV -> unscaled slabs; attention adds them, applies the row's deferred-norm factor and
       // RoPE, and writes the new K/V (k_attn.hip): one factor per attention block, not per
       // QKV tile
-      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv, dsplit_qkv, nullptr);
+      qa.S = proj_split(&Q[QS_QKV], xb, Ly.wqkv, B, QKVN, H, split_qkv, dsplit_qkv, nullptr, dwn_qkv);
     } else {
       // QKV GEMV epilogue: RoPE, q -> qkv rows, K/V -> paged cache
       GemvArgs ga{};
@@ -539,7 +546,7 @@ struct ms_engine {
       qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}};
     }
     if (!fused_qa) attn_decode(qa, kv, da);
-    resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm);
+    resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm, dwn_o);
     const RowScale rs_ffn = cur_rs;
     const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
     if (mlp_fused(&Q[QS_GU], &Q[QS_DOWN], B)) {
@@ -565,7 +572,7 @@ struct ms_engine {
       gg.rs = rs_ffn;
       proj(&Q[QS_GU], xb, Ly.wgu, hbuf, B, 2 * F, H, F, MS_GEMV_EPI_SWIGLU, &gg, K_GEMV, sizeof(f16_t));
     }
-    resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next);
+    resid_update(&Q[QS_DOWN], hbuf, Ly.wdown, B, F, split_down, dsplit_down, g_next, dwn_down);
   }
 
   // one transformer layer over T packed tokens (decode: T = B rows, one token each); on entry
@@ -874,6 +881,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_DSPLIT_QKV")) E.dsplit_qkv = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_O")) E.dsplit_o = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_DOWN")) E.dsplit_down = atoi(v);
+    if (const char* v = getenv("MS_DWN")) E.dwn_qkv = E.dwn_o = E.dwn_down = E.dwn_lm = atoi(v) == 8 ? 8 : 4;
     for (int* d : {&E.dsplit_qkv, &E.dsplit_o, &E.dsplit_down}) *d = std::min(std::max(*d, 1), (int)ms_engine::kMaxSplit);
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
@@ -1462,7 +1470,8 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     E.prof_begin(K_LMHEAD);
     // no row scale: r > 0 keeps every row's order (the logits themselves are never stored)
     // 4-wave blocks always: a 2004-block grid keeps two per CU (k_dgemm.hip kh)
-    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1);
+    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1,
+                 B <= 128 && E.V % 128 == 0 ? E.dwn_lm : 4);
     E.prof_end(K_LMHEAD);
     decode_tail(E, B, d, tiles);
     return;
@@ -1882,6 +1891,12 @@ int ms_set_attn_tuning(int32_t combine_grp, int32_t order) {
 int ms_set_dgemm_kh(int32_t kh) {
   if (kh != 1 && kh != 2) return MS_EINVAL;
   set_dgemm_kh(kh);
+  return MS_OK;
+}
+
+int ms_set_dgemm_wn(int32_t wn) {
+  if (wn != 4 && wn != 8) return MS_EINVAL;
+  set_dgemm_wn(wn);
   return MS_OK;
 }
 

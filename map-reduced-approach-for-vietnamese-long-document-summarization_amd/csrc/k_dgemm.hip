@@ -20,7 +20,7 @@
 
 namespace ms {
 
-constexpr int DBN = 64, DBK = 64;
+constexpr int DBK = 64;
 
 // KH = 2: an 8-wave block whose waves 4..7 take the upper 64 k of every 128-k step for the
 // same 64 weight rows, summed into waves 0..3 once at the end (acc(k half 0) + acc(k half 1),
@@ -35,29 +35,37 @@ int g_dgemm_kh = [] {
 
 void set_dgemm_kh(int kh) { g_dgemm_kh = kh == 2 ? 2 : 1; }
 int dgemm_kh_setting() { return g_dgemm_kh; }
+// WN = 8 (MS_DGEMM_WN, op-level tuning hook; engines pass it per launch): 8 weight-row groups,
+// 128 rows per block sharing one X image -- half the X bytes per weight byte.  Same sum order
+// as WN = 4 (every wave still covers its 16 rows over the whole K range in the same steps).
+static int g_dgemm_wn = [] {
+  const char* v = getenv("MS_DGEMM_WN");
+  return v && atoi(v) == 8 ? 8 : 4;
+}();
+void set_dgemm_wn(int wn) { g_dgemm_wn = wn == 8 ? 8 : 4; }
 
 // W ring depth: 3 K steps in flight at 2 blocks per CU; M > 128 (MT = 16) needs more
 // registers than 2 blocks per CU allow, so 1 block per CU with a deeper ring
 template <int MT, int KH> constexpr int dgemm_dpf() { return MT >= 16 || KH > 1 ? 6 : 3; }
 
-template <int MT, int EPI, int KH>
-__global__ __launch_bounds__(256 * KH, MT >= 16 || KH > 1 ? 1 : 2) void dgemm_kernel(const f16_t* __restrict__ X,
+template <int MT, int EPI, int KH, int WN>
+__global__ __launch_bounds__(64 * WN * KH, MT >= 16 || KH * WN > 4 ? 1 : 2) void dgemm_kernel(const f16_t* __restrict__ X,
                                                       const f16_t* __restrict__ W,
                                                       void* __restrict__ out, int M, int N, int K,
                                                       int ldk, int ldo, RowScale rs) {
-  constexpr int DPF = dgemm_dpf<MT, KH>();
-  constexpr int NT = 256 * KH, SK = DBK * KH;  // threads; k per step
+  constexpr int DPF = dgemm_dpf<MT, KH * WN / 4>();
+  constexpr int NT = 64 * WN * KH, SK = DBK * KH;  // threads; k per step
   // one X stage: KH half-images of XR rows x 128 B (16*MT rounded up to whole 16-B chunks per thread)
   constexpr int XR = 16 * MT < 32 ? 32 : 16 * MT;
   constexpr int XH = XR * DBK * 2, XB = XH * KH;
-  constexpr int XI = XR * 8 / 256;  // 16-B chunks of one stage per thread
-  constexpr int XCH = 4 * MT * 256 * 4;  // bytes of one [4 waves][MT][64 lanes][4] f32 exchange
+  constexpr int XC = XR * 8 * KH, XI = (XC + NT - 1) / NT;  // 16-B chunks of one stage; per thread
+  constexpr int XCH = WN * MT * 256 * 4;  // bytes of one [WN waves][MT][64 lanes][4] f32 exchange
   constexpr int SMEM = 2 * XB > KH * XCH ? 2 * XB : KH * XCH;
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave & 3, kh = wave >> 2;  // weight-row group, k half
+  const int wn = wave % WN, kh = wave / WN;  // weight-row group, k half
   const int fr = lane & 15, fg = lane >> 4;
-  const int n0 = blockIdx.x * DBN;
+  const int n0 = blockIdx.x * 16 * WN;
   const int kb = blockIdx.y * K;  // this split's K range in rows of length ldk
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) out = (float*)out + (size_t)blockIdx.y * M * ldo;
   const int nk = K / SK;
@@ -71,14 +79,14 @@ __global__ __launch_bounds__(256 * KH, MT >= 16 || KH > 1 ? 1 : 2) void dgemm_ke
   auto load_x = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int c = tid + NT * i, r = c / (8 * KH);
+      const int c = min(tid + NT * i, XC - 1), r = c / (8 * KH);
       xr[i] = ldg16(X + (size_t)min(r, M - 1) * ldk + kb + k0 + (c % (8 * KH)) * 8);
     }
   };
   auto store_x = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-      const int c = tid + NT * i, r = c / (8 * KH), cc = c % (8 * KH);
+      const int c = min(tid + NT * i, XC - 1), r = c / (8 * KH), cc = c % (8 * KH);
       *(uint4*)(smem + buf * XB + (cc >> 3) * XH + r * 128 + (((cc & 7) ^ (r & 7)) << 4)) = xr[i];
     }
   };
@@ -133,16 +141,16 @@ __global__ __launch_bounds__(256 * KH, MT >= 16 || KH > 1 ? 1 : 2) void dgemm_ke
   if constexpr (KH > 1) {
     // acc = ((acc(k part 0) + acc(part 1)) + acc(part 2)) + ...; the stages are free after the
     // loop's last sync
-    float* kx = (float*)smem;  // [KH - 1][4 waves][MT][64 lanes][4]
+    float* kx = (float*)smem;  // [KH - 1][WN waves][MT][64 lanes][4]
     if (kh)
 #pragma unroll
-      for (int m = 0; m < MT; ++m) *(f32x4*)&kx[(((kh - 1) * 4 + wn) * MT + m) * 256 + lane * 4] = acc[m];
+      for (int m = 0; m < MT; ++m) *(f32x4*)&kx[(((kh - 1) * WN + wn) * MT + m) * 256 + lane * 4] = acc[m];
     __syncthreads();
     if (!kh)
 #pragma unroll
       for (int p = 0; p < KH - 1; ++p)
 #pragma unroll
-        for (int m = 0; m < MT; ++m) acc[m] += *(const f32x4*)&kx[((p * 4 + wn) * MT + m) * 256 + lane * 4];
+        for (int m = 0; m < MT; ++m) acc[m] += *(const f32x4*)&kx[((p * WN + wn) * MT + m) * 256 + lane * 4];
   }
 
   // epilogue (waves 0..3): acc[m][j] = C[row m*16 + 4 fg + j][col n0 + 16 wn + fr]; rows scaled
@@ -157,7 +165,7 @@ __global__ __launch_bounds__(256 * KH, MT >= 16 || KH > 1 ? 1 : 2) void dgemm_ke
   if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
     // waves 2q / 2q+1 hold the gate / up tile of the same 16 features: pair through LDS
     // (a region of its own: the k-half exchange may still be read by a slower wave)
-    float* xch = (float*)(smem + (KH - 1) * XCH);  // [4 waves][MT][64 lanes][4]
+    float* xch = (float*)(smem + (KH - 1) * XCH);  // [WN waves][MT][64 lanes][4]
     if (!kh)
 #pragma unroll
       for (int m = 0; m < MT; ++m) *(f32x4*)&xch[((wn * MT + m) * 64 + lane) * 4] = acc[m];
@@ -209,22 +217,25 @@ __global__ __launch_bounds__(256 * KH, MT >= 16 || KH > 1 ? 1 : 2) void dgemm_ke
 
 // kh 0 = the library setting where it applies (M <= 128, K % (128 S) == 0), else 1
 static int dgemm_kh_for(int M, int K, int S) { return g_dgemm_kh == 2 && M <= 128 && K % (S * 2 * DBK) == 0 ? 2 : 1; }
+static int dgemm_wn_for(int M, int N, int kh) { return g_dgemm_wn == 8 && kh == 1 && M <= 128 && N % 128 == 0 ? 8 : 4; }
 
-bool dgemm_supported(int M, int N, int K, int S, int epi, int kh) {
+bool dgemm_supported(int M, int N, int K, int S, int epi, int kh, int wn) {
   if (!kh) kh = dgemm_kh_for(M, K, S);
-  if (M < 1 || M > (kh > 1 ? 128 : 256) || N % 64 || S < 1 || K % (S * DBK * kh)) return false;
+  if (!wn) wn = dgemm_wn_for(M, N, kh);
+  if (wn != 4 && (wn != 8 || kh != 1 || M > 128)) return false;
+  if (M < 1 || M > (kh > 1 ? 128 : 256) || N % (16 * wn) || S < 1 || K % (S * DBK * kh)) return false;
   if (epi == MS_GEMV_EPI_ROPE_KV) return false;
   if (S > 1 && epi != MS_GEMV_EPI_STORE_F32) return false;
   return true;
 }
 
-template <int MT, int KH>
+template <int MT, int KH, int WN = 4>
 static void dgemm_go(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo,
                      int epi, const RowScale& rs, hipStream_t s) {
-  const dim3 grid(N / DBN, S), blk(256 * KH);
+  const dim3 grid(N / (16 * WN), S), blk(64 * WN * KH);
   const int Ks = K / S;
   switch (epi) {
-#define DG(E_) MS_LAUNCH((dgemm_kernel<MT, E_, KH>), grid, blk, 0, s, X, W, out, M, N, Ks, K, ldo, rs)
+#define DG(E_) MS_LAUNCH((dgemm_kernel<MT, E_, KH, WN>), grid, blk, 0, s, X, W, out, M, N, Ks, K, ldo, rs)
     case MS_GEMV_EPI_STORE_F16: DG(MS_GEMV_EPI_STORE_F16); break;
     case MS_GEMV_EPI_ADD_F32: DG(MS_GEMV_EPI_ADD_F32); break;
     case MS_GEMV_EPI_SWIGLU: DG(MS_GEMV_EPI_SWIGLU); break;
@@ -236,15 +247,23 @@ static void dgemm_go(const f16_t* X, const f16_t* W, void* out, int M, int N, in
 
 // rs: the deferred RMSNorm scale of the output rows, one-tile partials only (or null)
 void launch_dgemm(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  hipStream_t s, const RowScale* rs_in, int kh) {
+                  hipStream_t s, const RowScale* rs_in, int kh, int wn) {
   if (!kh) kh = dgemm_kh_for(M, K, S);
-  if (!dgemm_supported(M, N, K, S, epi, kh)) return;  // callers check
+  if (!wn) wn = dgemm_wn_for(M, N, kh);
+  if (!dgemm_supported(M, N, K, S, epi, kh, wn)) return;  // callers check
   RowScale rs{};
   if (rs_in && rs_in->ssq && epi != MS_GEMV_EPI_ARGMAX) {  // argmax: r > 0 keeps the order
     if (rs_in->tiles != 1) return;  // callers pass one-tile statistics (a norm kernel's)
     rs = *rs_in;
   }
   const int mt = (M + 15) / 16;
+  if (wn == 8) {  // 128 weight rows per block (KH = 1, M <= 128)
+    if (mt <= 1) dgemm_go<1, 1, 8>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+    else if (mt <= 2) dgemm_go<2, 1, 8>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+    else if (mt <= 4) dgemm_go<4, 1, 8>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+    else dgemm_go<8, 1, 8>(X, W, out, M, N, K, S, ldo, epi, rs, s);
+    return;
+  }
   if (kh > 1) {  // the k-half block (M <= 128)
     if (mt <= 1) dgemm_go<1, 2>(X, W, out, M, N, K, S, ldo, epi, rs, s);
     else if (mt <= 2) dgemm_go<2, 2>(X, W, out, M, N, K, S, ldo, epi, rs, s);

@@ -129,6 +129,8 @@ void set_attn_tuning(int combine_grp, int order);
 // large-batch skinny GEMM: 1 = 4-wave blocks, 2 = 8-wave blocks with the K step split in halves
 // (S = 1 launches; a different but M-independent sum order)
 void set_dgemm_kh(int kh);
+// op-level skinny GEMM: weight-row groups per block (4 or 8; engines choose per launch)
+void set_dgemm_wn(int wn);
 // M <= 64 decode variant (weight streaming); gemv_supported() says whether a shape fits.
 // Epilogues: the four of launch_gemm plus ROPE_KV (QKV with rope-permuted Q/K rows).
 enum {
@@ -213,9 +215,11 @@ void launch_gemv_ex(const f16_t* X, const f16_t* W, void* out, int M, int N, int
 // kh: 1 = 4-wave blocks, 2 = 8-wave blocks splitting each 128-k step in two k halves (then
 // K % (128 S) == 0 and M <= 128), 0 = the library setting (set_dgemm_kh) where it applies
 // (M <= 128, K % (128 S) == 0), else 1
-bool dgemm_supported(int M, int N, int K, int S, int epi, int kh = 0);
+// wn: weight-row groups per block, 4 (64 rows) or 8 (128 rows; kh 1, M <= 128, N % 128 == 0;
+// the same bits as 4), 0 = the op-level setting (MS_DGEMM_WN) where it applies, else 4
+bool dgemm_supported(int M, int N, int K, int S, int epi, int kh = 0, int wn = 0);
 void launch_dgemm(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
-                  hipStream_t s, const RowScale* rs = nullptr, int kh = 0);
+                  hipStream_t s, const RowScale* rs = nullptr, int kh = 0, int wn = 0);
 int dgemm_kh_setting();
 
 // ---- ggml K-quant weights (k_qgemv.hip)

@@ -33,7 +33,7 @@ EXPORTED = (
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_dgemm", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
-    "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant", "ms_set_qgemv_gs", "ms_set_attn_tuning", "ms_set_dgemm_kh",
+    "ms_op_argmax", "ms_op_argmax_partials", "ms_set_gemm_variant", "ms_set_qgemv_gs", "ms_set_attn_tuning", "ms_set_dgemm_kh", "ms_set_dgemm_wn",
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
     "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
@@ -129,6 +129,7 @@ def load_at(path: str, ab: bool = True) -> C.CDLL:
         "ms_set_qgemv_gs": (i32, [i32]),
         "ms_set_attn_tuning": (i32, [i32, i32]),
         "ms_set_dgemm_kh": (i32, [i32]),
+        "ms_set_dgemm_wn": (i32, [i32]),
         "ms_op_argmax": (i32, [vp, i32, i32, vp, vp]),
         "ms_op_argmax_partials": (i32, [vp, i32, i32, vp, vp]),
         "ms_weight_regions": (i32, [vp, C.POINTER(vp), C.POINTER(i64), i32]),

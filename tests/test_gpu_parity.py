@@ -222,6 +222,33 @@ def test_dgemm_rows_independent_of_batch(lib, dev, dgemm_kh, N, K, S, epi):
         assert torch.equal(outs[M][:, :24], outs[24]), M
 
 
+@pytest.mark.parametrize("M", [17, 64, 128])
+@pytest.mark.parametrize("N,K,S,epi", [(5120, 3072, 6, L.MS_EPI_STORE_F32), (3072, 8192, 8, L.MS_EPI_STORE_F32),
+                                       (4096, 3072, 1, L.MS_EPI_ARGMAX), (2048, 768, 1, L.MS_EPI_SWIGLU)])
+def test_dgemm_128_row_blocks_bit_identical(lib, dev, M, N, K, S, epi):
+    """128 weight rows per skinny-GEMM block (ms_set_dgemm_wn(8), what engines run for QKV,
+    down and the lm_head) give the same bits as 64-row blocks: each wave's rows, K steps and
+    MFMA order are the same."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + S + epi)
+    X = _f16(torch.randn(M, K, generator=g)).to(dev)
+    W = _f16(torch.randn(N, K, generator=g) * 0.05).to(dev)
+    ldo = N // 2 if epi == L.MS_EPI_SWIGLU else (N // 16 if epi == L.MS_EPI_ARGMAX else N)
+    L.check(lib.ms_set_dgemm_kh(1))
+    res = []
+    try:
+        for wn in (4, 8):
+            L.check(lib.ms_set_dgemm_wn(wn))
+            o = torch.full((S * M * N * 2,), float("nan"), device=dev)
+            L.check(lib.ms_op_dgemm(X.data_ptr(), W.data_ptr(), o.data_ptr(), M, N, K, S, ldo, epi, _stream()))
+            torch.cuda.synchronize()
+            res.append(o.cpu())
+    finally:
+        L.check(lib.ms_set_dgemm_wn(4))
+        L.check(lib.ms_set_dgemm_kh(2))
+    n = S * M * ldo * (2 if epi == L.MS_EPI_ARGMAX else 1) // (2 if epi == L.MS_EPI_SWIGLU else 1)
+    assert torch.equal(res[0][:n], res[1][:n])
+
+
 @pytest.mark.parametrize("M", [1, 8, 16])
 @pytest.mark.parametrize("N,K,S", [(3072, 3072, 4), (3072, 8192, 4), (768, 2048, 2), (256, 768, 3),
                                    (3072, 8192, 8)])

@@ -112,7 +112,7 @@ def bench_dgemm(lib):
                                     ("lm_head", 128256, 3072, 5, (1,))]:
         Ws = [torch.randn(N, K, device=dev).to(torch.float16) * 0.02
               for _ in range(max(2, -(-512 * 2**20 // (N * K * 2))))]
-        for M in (32, 64, 128, 256):
+        for M in (8, 16, 32, 64, 128, 256):
             X = torch.randn(M, K, device=dev).to(torch.float16)
             out = torch.zeros(8 * M * N, device=dev)
             wbytes = N * K * 2
