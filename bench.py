@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "map-phase chunks/sec (2k-tok chunk, 256-tok summary) at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: 8.0 TB/s spec
+DGEMM_MIN = 24              # engines of >= 24 slots decode on the skinny GEMM (engine.cpp dgemm_min)
 F16_PEAK_TFLOPS = 2500.0    # dense fp16 (= bf16) MFMA (MI355X_MICROARCH.md chip table)
 CHUNKS_PER_DOC = 8          # BASELINE.json configs[0..2]: a 16k-token doc in 2k chunks
 
@@ -180,16 +181,24 @@ def _physical_cores():
 
 
 def pmc_traffic(weights, B, prompt_len):
-    """HBM bytes per GEMV launch from the committed rocprofv3 --pmc passes of this same
-    workload (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic_from_pmc.py, run by
-    tools/gpu_round.sh), or (None, None) when none was taken at this B and prompt length.
-    PMC counters cannot be read inside a timed run: this is the profiler's number."""
+    """HBM bytes per weight-stream launch from the committed rocprofv3 --pmc passes of the
+    same launches (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic_from_pmc.py, run by
+    tools/gpu_round.sh / tools/gpu_r5af.sh), or (None, None) when none was taken.  B is the
+    engine's max_batch = the rows in flight; a pass matches when its rows (min(chunks,
+    max_batch)), hence its decode regime (skinny GEMM at >= DGEMM_MIN rows, else GEMV), and
+    its prompt length are this run's.  PMC counters cannot be read inside a timed run: this
+    is the profiler's number."""
     import glob
-    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{weights}.json")))
+    key = (B, B >= DGEMM_MIN, prompt_len)
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{weights}*.json")))
     for h in reversed(hits):
         d = json.load(open(h))
         wl = d.get("workload", {})
-        if wl.get("chunks_per_gpu") == B and wl.get("prompt_len") == prompt_len:
+        c = wl.get("chunks_per_gpu")
+        if c is None:
+            continue
+        m = wl.get("max_batch", c)
+        if (min(c, m), m >= DGEMM_MIN, wl.get("prompt_len")) == key:
             return d["traffic_bytes_per_launch"], os.path.relpath(h, ROOT)
     return None, None
 
@@ -363,9 +372,11 @@ def main():
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
             traffic, traffic_src = pmc_traffic(args.weights, B, args.prompt_len)
+            skinny = not quant and B >= DGEMM_MIN
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
-                    "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else "gemv_kernel (fp16")
+                    "kernel": ("qgemv_kernel (Q4_K/Q6_K" if quant else
+                               "dgemm_kernel (fp16 skinny GEMM, >= 24 slots:" if skinny else "gemv_kernel (fp16")
                               + " decode weight stream: QKV/O/gate-up/down projections + lm_head)",
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
