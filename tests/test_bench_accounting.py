@@ -110,3 +110,15 @@ def test_bench_rank_logic_world2_gloo():
     for (d, c), ids in got.items():
         want = bench.synthetic_chunks(1, 32, d, 128256, 128000, first_chunk=c)[0][::-1][:4]
         assert ids == want.tolist()
+
+
+def test_pmc_traffic_matches_rows_and_regime():
+    """The roofline's PMC traffic is quoted only from a pass over the same launches: the same
+    rows in flight (the engine's max_batch), hence the same decode regime (GEMV below 24 rows,
+    skinny GEMM at >= 24), and the same prompt length."""
+    t8, src8 = bench.pmc_traffic("f16", 8, 2048)
+    assert src8 and src8.endswith("pmc_traffic_f16.json") and t8 > 57_000_000
+    t128, src128 = bench.pmc_traffic("f16", 128, 2048)
+    assert src128 and src128.endswith("pmc_traffic_f16_b128.json") and t128 > t8
+    assert bench.pmc_traffic("f16", 64, 2048) == (None, None)  # no pass at 64 rows
+    assert bench.pmc_traffic("f16", 8, 1024) == (None, None)
