@@ -877,7 +877,9 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
-    E.dgemm_kh = cfg->max_batch <= 128 ? dgemm_kh_setting() : 1;
+    // (the k-half block steps 128 k at a time: hidden sizes that are not a multiple of 128
+    // keep the 4-wave block)
+    E.dgemm_kh = cfg->max_batch <= 128 && E.H % 128 == 0 ? dgemm_kh_setting() : 1;
     if (const char* v = getenv("MS_DSPLIT_QKV")) E.dsplit_qkv = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_O")) E.dsplit_o = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_DOWN")) E.dsplit_down = atoi(v);
