@@ -52,29 +52,22 @@ def synthetic_chunks(n, prompt_len, doc, vocab, bos, seed=0, first_chunk=0):
     return out
 
 
-def gemv_bytes_per_step(cfg, B, qkv_fused=False):
+def gemv_bytes_per_step(cfg, B):
     """Algorithmic HBM bytes of one decode step's layer projections: every weight matrix
-    once + the B activation rows in/out (SURVEY.md §8d weight term, without lm_head).
-    qkv_fused: the QKV projection runs inside the fused QKV + attention launch (k_qkvattn.hip),
-    so the GEMV launches stream O / gate-up / down only."""
+    once + the B activation rows in/out (SURVEY.md §8d weight term, without lm_head)."""
     H, D, F = cfg.hidden, cfg.head_dim, cfg.ffn
     qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
     w = 2 * (qkv * H + H * cfg.n_heads * D + 2 * F * H + H * F)
     act = 2 * B * (H + qkv + cfg.n_heads * D + H + H + F + F + H) + 4 * B * H * 4
-    if qkv_fused:
-        w -= 2 * qkv * H
-        act -= 2 * B * (H + qkv)
     return cfg.n_layers * (w + act)
 
 
-def qkv_attn_bytes_per_launch(cfg, B, kv_keys):
-    """The fused QKV + attention launch of one layer: the QKV weights, its B input rows, the
-    fp32 projection handed off (written once, read once), and the K/V of kv_keys cached keys
-    summed over the batch (SURVEY.md §8d's KV-read term) plus the new tokens' K/V."""
-    H, D = cfg.hidden, cfg.head_dim
-    qkv = (cfg.n_heads + 2 * cfg.n_kv_heads) * D
-    kv_tok = 2 * cfg.n_kv_heads * D * 2
-    return 2 * qkv * H + 2 * B * H + 2 * 4 * B * qkv + kv_keys * kv_tok + B * kv_tok
+def persist_bytes_per_launch(cfg, B, kv_read_tokens):
+    """The persistent decode step (k_persist.hip), one launch = every layer of one decode step:
+    each layer's weights once + the B activation rows in / out (gemv_bytes_per_step), the K/V of
+    the cached keys it attends (SURVEY.md §8d's KV-read term; kv_read_tokens = keys summed over
+    the batch rows, all layers) and the new tokens' K/V rows it writes."""
+    return gemv_bytes_per_step(cfg, B) + kv_read_tokens * cfg.kv_bytes_per_token + B * cfg.kv_bytes_per_token
 
 
 def _q4_k_m_bytes_per_weight(tensor, layer, n_layers):
@@ -180,7 +173,7 @@ def _physical_cores():
         return None
 
 
-def pmc_traffic(weights, B, prompt_len):
+def pmc_traffic(weights, B, prompt_len, kernel="gemv"):
     """HBM bytes per weight-stream launch from the committed rocprofv3 --pmc passes of the
     same launches (FETCH_SIZE x2 + WRITE_SIZE, tools/traffic_from_pmc.py, run by
     tools/gpu_round.sh / tools/gpu_r5af.sh), or (None, None) when none was taken.  B is the
@@ -193,6 +186,8 @@ def pmc_traffic(weights, B, prompt_len):
     hits = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_traffic_{weights}*.json")))
     for h in reversed(hits):
         d = json.load(open(h))
+        if d.get("kernel_class", "gemv") != kernel:  # the persistent step's passes say "persist"
+            continue
         wl = d.get("workload", {})
         c = wl.get("chunks_per_gpu")
         if c is None:
@@ -351,23 +346,46 @@ def main():
                  "batch_invariant_chunk0": alone == outs[0][0]}
         assert same and full and check["batch_invariant_chunk0"], check
 
-    roof = roof_qa = None
+    roof = roof_lm = None
     if not args.no_roofline:
-        # Roofline of the dominant kernel class (the decode weight stream): one more map
-        # step with HIP events bracketing every GEMV launch on the engine's stream.  It
-        # runs after the timed region because an event pair per launch (113 per decode
-        # step) costs ~0.6 ms/step and would distort `value`.
+        # Roofline of the dominant kernel: one more map step with HIP events bracketing every
+        # decode launch of its class on the engine's stream (an event pair per launch would
+        # distort `value`, so this runs after the timed region).  Engines of <= 8 slots on fp16
+        # weights run every layer of a decode step as ONE persistent launch (k_persist.hip):
+        # its bytes are the layers' weights + the K/V it reads and writes; otherwise the class is
+        # the per-projection weight stream (GEMV / skinny GEMM / K-quant GEMV) + the lm_head.
         eng.reset_stats()
-        eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD) | (1 << L.K_QKV_ATTN))
+        eng.set_profiling((1 << L.K_GEMV) | (1 << L.K_LMHEAD) | (1 << L.K_PERSIST))
         eng.generate(chunks[:min(len(chunks), B)], num_predict=min(args.gen_len, 64), ignore_eos=True)
         eng.set_profiling(0)
         sp = eng.stats()
-        launches = sp["kernel_launches"][L.K_GEMV] + sp["kernel_launches"][L.K_LMHEAD]
-        n_qa = sp["kernel_launches"][L.K_QKV_ATTN]
-        if launches:
+        bstep = sp["decode_tokens"] / max(sp["decode_steps"], 1)
+        n_pk = sp["kernel_launches"][L.K_PERSIST]
+        n_lm = sp["kernel_launches"][L.K_LMHEAD]
+        launches = sp["kernel_launches"][L.K_GEMV] + n_lm
+        if n_pk:
+            pk_s = sp["kernel_ms"][L.K_PERSIST] / 1e3
+            kv_read = sp["decode_kv_tokens"] * 1.0  # keys attended per layer, summed over steps and rows
+            pk_bytes = persist_bytes_per_launch(cfg, bstep, 0) * n_pk + kv_read * cfg.kv_bytes_per_token
+            ach = pk_bytes / pk_s / 1e9
+            traffic, traffic_src = pmc_traffic(args.weights, B, args.prompt_len, "persist")
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                    "kernel": "decode_step_kernel (persistent: all 28 layers of a decode step in one launch -- "
+                              "QKV/O/gate-up/down weights + K/V reads and writes)",
+                    "bytes_per_launch": int(pk_bytes / n_pk),
+                    "avg_launch_us": round(pk_s / n_pk * 1e6, 2),
+                    "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}
+            if n_lm:
+                lm_s = sp["kernel_ms"][L.K_LMHEAD] / 1e3
+                lm_b = lm_head_bytes_per_step(cfg, bstep, quant) * n_lm
+                roof_lm = {"bound": "hbm", "achieved": round(lm_b / lm_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(lm_b / lm_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "kernel": "gemv_kernel (lm_head + argmax partials)",
+                           "bytes_per_launch": int(lm_b / n_lm), "avg_launch_us": round(lm_s / n_lm * 1e6, 2)}
+        elif launches:
             gemv_s = (sp["kernel_ms"][L.K_GEMV] + sp["kernel_ms"][L.K_LMHEAD]) / 1e3
-            bstep = sp["decode_tokens"] / max(sp["decode_steps"], 1)
-            per_step = (qgemv_bytes_per_step(cfg, bstep) if quant else gemv_bytes_per_step(cfg, bstep, n_qa > 0)) \
+            per_step = (qgemv_bytes_per_step(cfg, bstep) if quant else gemv_bytes_per_step(cfg, bstep)) \
                 + lm_head_bytes_per_step(cfg, bstep, quant)
             bytes_total = per_step * sp["decode_steps"]
             ach = bytes_total / gemv_s / 1e9
@@ -381,20 +399,6 @@ def main():
                     "bytes_per_launch": int(bytes_total / launches),
                     "avg_launch_us": round(gemv_s / launches * 1e6, 2),
                     "method": "hipExtLaunchKernelGGL start/stop events per launch, one extra untimed map step"}
-            if n_qa:
-                # the fused QKV + attention launch (k_qkvattn.hip) streams the QKV weights and the
-                # K/V together: its own HBM roofline entry; the GEMV class above excludes QKV
-                roof["kernel"] = "gemv_kernel (fp16 decode weight stream: O/gate-up/down projections + lm_head)"
-                qa_s = sp["kernel_ms"][L.K_QKV_ATTN] / 1e3
-                qa_bytes = (qkv_attn_bytes_per_launch(cfg, bstep, 0) * n_qa
-                            + sp["decode_kv_tokens"] * cfg.n_layers * 2 * cfg.n_kv_heads * cfg.head_dim * 2)
-                qa_gbs = qa_bytes / qa_s / 1e9
-                roof_qa = {"bound": "hbm", "achieved": round(qa_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                           "frac": round(qa_gbs / HBM_PEAK_GBS, 4), "kernel": "qkv_attn_kernel (fused QKV "
-                           "projection + decode attention, one launch per layer)",
-                           "bytes_per_launch": int(qa_bytes / n_qa), "avg_launch_us": round(qa_s / n_qa * 1e6, 2),
-                           "method": "QKV weights + fp32 hand-off + K/V read (decode_kv_tokens) per event-timed "
-                                     "launch, the same extra untimed map step"}
     # whole-phase rooflines from the timed run's own event-timed prefill / decode passes
     pre_flops = prefill_flops_per_chunk(cfg, args.prompt_len) * n_local * args.steps
     pre_tf = pre_flops / (st["prefill_ms"] / 1e3) / 1e12 if st["prefill_ms"] else None
@@ -436,6 +440,8 @@ def main():
                       "decode_steps": st["decode_steps"],
                       "summary_tokens_per_step": int(sum(len(x) for x in outs[0])),
                       "graphs_built": st["graphs_built"],
+                      "persist_steps": st["persist_steps"],
+                      "persist_fallbacks": st["persist_fallbacks"],
                       "decode_ms_per_decode_step": round(st["decode_ms"] / max(st["decode_steps"], 1), 4),
                       "gather_ms_per_step": round(gather_s[0] / args.steps * 1e3, 3),
                       "weight_load_s": round(t_load, 3),
@@ -444,7 +450,7 @@ def main():
         "roofline": roof,
         "roofline_prefill": roof_pre,
         "roofline_decode": roof_dec,
-        "roofline_qkv_attn": roof_qa,
+        "roofline_lm_head": roof_lm,
         "check": check,
         "cpu_baseline": None,
     }

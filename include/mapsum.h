@@ -117,13 +117,16 @@ typedef struct ms_stats {
   double kernel_ms[8];          /* per kernel class, when profiling is on:
                                    0 gemm(prefill) 1 attn_prefill 2 gemv(decode)
                                    3 attn_decode 4 lm_head 5 norm/rope/misc
-                                   6 qkv_attn (the fused QKV projection + decode
-                                   attention of <= 8-slot engines)              */
+                                   6 persist (the decode step's layers as one
+                                   persistent launch, <= 8-slot engines)        */
   int64_t kernel_launches[8];
   int64_t decode_kv_tokens;     /* sum over decode steps and rows of the keys attended
                                    (the KV-read term of SURVEY.md §8d's decode bytes)  */
   int64_t graphs_built;         /* decode hipGraphs captured + instantiated (the cache keeps
                                    at most 64, least recently used evicted)            */
+  int64_t persist_fallbacks;    /* decode runs recomputed with the per-layer launches after a
+                                   hand-off of the persistent step timed out (expected 0)  */
+  int64_t persist_steps;        /* decode steps that ran the persistent launch             */
 } ms_stats;
 
 typedef struct ms_engine ms_engine;
@@ -187,9 +190,20 @@ int ms_set_profiling(ms_engine* e, uint32_t class_mask);
 int ms_trace_push(const char* name);
 int ms_trace_pop(void);
 int ms_synchronize(ms_engine* e);
-/* diagnostic: the fused QKV + attention launch's phase stamps of its latest launch, [256][16]
-   s_memrealtime ticks (100 MHz), recorded only under MS_QA_STAMPS=1 (tools/qa_stamps.py) */
-int ms_debug_qa_stamps(uint64_t* out, int32_t n);
+/* the decode step's layers as ONE persistent launch (k_persist.hip; engines of <= 8 slots on
+   fp16 Llama-3.2-3B weights, bit-identical to the per-layer launches): on (1, the default, also
+   MS_PERSIST) or off (0).  Returns 1 when this engine supports it, 0 when it never runs it. */
+int ms_set_persist(ms_engine* e, int32_t on);
+/* test hook: copy `bytes` from byte `offset` of an engine buffer to host memory (after the
+   engine's streams are idle) */
+#define MS_DBG_KPOOL 0          /* K cache [layer][page][kv_head][64][head_dim] fp16 */
+#define MS_DBG_VPOOL 1          /* V cache, same layout */
+#define MS_DBG_DECODE_LOGITS 2  /* the decode lm_head output (argmax partials {max, id} per 16 columns) */
+#define MS_DBG_DECODE_X 3       /* the decode residual [max_batch][hidden] fp32 */
+int ms_debug_read(ms_engine* e, int32_t which, int64_t offset, void* host, int64_t bytes);
+/* diagnostic: the persistent step's in-kernel timeline of its latest launch, [256][28][16]
+   s_memrealtime ticks (100 MHz), recorded only under MS_PK_STAMPS=1 (tools/pk_stamps.py) */
+int ms_debug_pk_stamps(uint64_t* out, int32_t n);
 /* diagnostic: decode attention v2's per-block phase stamps of its latest launch, [1024][32]
    (entry, XCC / HW id, prologue, per-wave S and P.V done, partial stored), recorded only under
    MS_A2_STAMPS=1 (tools/a2_stamps.py) */

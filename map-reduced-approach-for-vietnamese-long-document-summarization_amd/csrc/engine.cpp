@@ -68,7 +68,7 @@ struct MsError : std::runtime_error {
     if (!(cond)) throw MsError((code), (msg));        \
   } while (0)
 
-enum KClass { K_GEMM = 0, K_ATTN_PREFILL = 1, K_GEMV = 2, K_ATTN_DECODE = 3, K_LMHEAD = 4, K_MISC = 5, K_QKV_ATTN = 6 };
+enum KClass { K_GEMM = 0, K_ATTN_PREFILL = 1, K_GEMV = 2, K_ATTN_DECODE = 3, K_LMHEAD = 4, K_MISC = 5, K_PERSIST = 6 };
 
 struct Seq {
   uint64_t tag = 0;
@@ -161,21 +161,6 @@ struct ms_engine {
   bool attn2_ok(int B, int max_len) const {
     return attn_v2 && slot_major && attn_decode2_supported(B, Hq, Hk, max_len, attn_ppb);
   }
-  // the QKV projection and decode attention as one launch (k_qkvattn.hip, MS_QKV_ATTN=1): engines
-  // of <= 8 slots on fp16 QKV weights with the v2 attention plan; chosen per engine at creation
-  // (qkv_attn_supported at max_batch / max_ctx holds for every step) and bit-identical to the
-  // split-6 GEMV + v2 attention it replaces.  Opt-in: measured SLOWER, 32.4-35.4 vs 8.2 + 18.4 us
-  // per layer (decode 2.25-2.33 vs 2.09 ms per step, profiles/r05/v6_*): a CU's memory
-  // operations retire in order across its waves, so the hand-off (publish drain, arrival, poll,
-  // prologue reads) either queues behind the K/V pages in flight on its CU or the pages wait for
-  // the hand-off -- in-kernel stamps put publish -> poll at 6-7 us, against ~1.5 us for a kernel
-  // boundary.  qa_used: a launch since the last error check (shares the hand-off timeout flag
-  // mlp_sync_d[16]; its counters are mlp_sync_d[32..48])
-  bool qkv_attn = false, qa_used = false;
-  bool qkv_attn_on(const QSlot* q, int B, int max_len) const {
-    return qkv_attn && attn_slabs && !(q && q->ready()) && attn2_ok(B, max_len) &&
-           qkv_attn_supported(B, cfg.max_batch, H, Hq, Hk, max_len, attn_ppb, split_qkv);
-  }
   void attn_decode(const DecodeQKV& qa, const KVView& kv, const DecodeAttnArgs& da) {
     prof_begin(K_ATTN_DECODE);
     if (attn2_ok(da.B, da.max_len))
@@ -192,18 +177,25 @@ struct ms_engine {
   // lm_head outputs instead.  Chosen per engine (MS_RESID_FUSED=0: split-K slabs + norm
   // launches, the large-regime form; K-quant engines take it too, below: qresid).
   bool resid_fuse = true, has_quant = false;
-  // the layer's decode MLP as one launch (k_mlp.hip: gate/up, a chip-wide hand-off of h, down
-  // + residual; bit-identical to the two launches), engines of <= 8 slots on fp16 MLP weights:
-  // opt-in (MS_MLP_FUSED=1) -- measured no faster than the two launches, 2.158 vs 2.130 ms per
-  // decode step at B = 8 (profiles/r04/v13_*).  mlp_sync_d: [0..1] counters, [16] timeout flag
-  bool mlp_fuse = false, mlp_used = false;
   // decode_tail_kernel: the step's greedy ids, argument advance and next embedding in one launch
   bool tail_fuse = true;
-  unsigned* mlp_sync_d = nullptr;
-  unsigned* mlp_err_h = nullptr;
-  bool mlp_fused(const QSlot* gu, const QSlot* dn, int B) const {
-    return mlp_fuse && !(gu && gu->ready()) && resid_fused(gu) && resid_fused(dn) && cfg.max_batch <= 8 &&
-           mlp_decode_supported(B, H, F, H / resid_rt);
+  // The decode step's layers as ONE persistent launch (k_persist.hip, MS_PERSIST / ms_set_persist;
+  // off by default until it measures faster than the launches):
+  // engines of <= 8 slots on fp16 Llama-3.2-3B weights in the residual-fused / v2-attention
+  // regime, bit-identical to the per-layer launches below.  Chosen per engine (persist_ok at
+  // ms_create) and per run (no profiling mask, no prefill overlap: every workgroup must be
+  // resident); a hand-off timeout sets pk_err_d, and decode_run recomputes the run with the
+  // launches and turns the persistent step off for the engine.
+  bool persist = false, persist_ok = false, pk_used = false;
+  int n_cu = 0, nsplit_ws = 1;
+  unsigned* pk_sync = nullptr;   // [persist_sync_words(L)] zero between launches
+  unsigned* pk_err_d = nullptr;  // timeout flag
+  unsigned* pk_err_h = nullptr;  // pinned copy
+  f16_t* pk_xg2 = nullptr;       // [max_batch][H] gate/up input
+  float* pk_ssq2 = nullptr;      // [256][max_batch] its statistics
+  bool persist_on(int B) const {
+    return persist && persist_ok && !overlap && B >= 1 && B <= cfg.max_batch && !has_quant &&
+           attn2_ok(B, max_pages * kPage) && attn_slabs && resid_fused(nullptr) && split_qkv == 6;
   }
   int resid_rt = 12;
   // K-quant O / down with the same epilogue (the Q-GEMV on resid_rt-row tiles; MS_QRESID=0:
@@ -517,16 +509,7 @@ struct ms_engine {
     const auto& Q = lq[l];
     const RowScale rs_attn = cur_rs;
     DecodeQKV qa{nullptr, slabs, 0, cos_tab, sin_tab, rs_attn};
-    const bool fused_qa = qkv_attn_on(&Q[QS_QKV], B, da.max_len);
-    if (fused_qa) {
-      // one launch: the QKV rows (slab 0 holds the folded split-6 sums) and attention
-      qa.S = 1;
-      prof_begin(K_QKV_ATTN);
-      launch_qkv_attn(xb, Ly.wqkv, slabs, qa, attn, Hq, Hk, kv, da, attn_ws, attn_ppb, mlp_sync_d + 32,
-                      mlp_sync_d + 16, stream);
-      prof_end(K_QKV_ATTN);
-      qa_used = true;
-    } else if (attn_slabs) {
+    if (attn_slabs) {
       // QKV -> unscaled slabs; attention adds them, applies the row's deferred-norm factor and
       // RoPE, and writes the new K/V (k_attn.hip): one factor per attention block, not per
       // QKV tile
@@ -545,22 +528,10 @@ struct ms_engine {
       proj(&Q[QS_QKV], xb, Ly.wqkv, qkv, B, QKVN, H, QKVN, MS_GEMV_EPI_ROPE_KV, &ga, K_GEMV);
       qa = DecodeQKV{qkv, nullptr, 0, cos_tab, sin_tab, RowScale{}};
     }
-    if (!fused_qa) attn_decode(qa, kv, da);
+    attn_decode(qa, kv, da);
     resid_update(&Q[QS_O], attn, Ly.wo, B, Hq * D, split_o, dsplit_o, Ly.ffn_norm, dwn_o);
     const RowScale rs_ffn = cur_rs;
     const f16_t* g_next = l + 1 < L ? layers[l + 1].attn_norm : final_norm;
-    if (mlp_fused(&Q[QS_GU], &Q[QS_DOWN], B)) {
-      // xb / ssq are the gate/up input AND the down epilogue's outputs: every workgroup has
-      // consumed them before the hand-off that precedes the first write
-      prof_begin(K_GEMV);
-      launch_mlp_decode(xb, Ly.wgu, Ly.wdown, hbuf, x, B, H, F, rs_ffn, ssq, g_next, xb, mlp_sync_d,
-                        mlp_sync_d + 16, stream);
-      prof_end(K_GEMV);
-      mlp_used = true;
-      pending_split = 0;
-      cur_rs = make_row_scale(ssq, H / resid_rt, H, cfg.norm_eps);
-      return;
-    }
     if (large(B)) {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
@@ -865,8 +836,12 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_ATTN_V2")) E.attn_v2 = atoi(v) != 0;
     if (const char* v = getenv("MS_ATTN_TICKET")) E.attn_ticket = atoi(v) != 0;
     E.attn_cnt = E.dalloc<unsigned>((size_t)cfg->max_batch * E.Hk, true);
-    E.attn_ws = (float*)E.dalloc<char>(std::max(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx),
-                                                attn_decode2_workspace_bytes(cfg->max_batch, E.Hq, cfg->max_ctx,
+    // decode_run sets the split grid from the longest sequence rounded UP to 256 keys, which can
+    // pass max_ctx when max_ctx is not a multiple of 256: size both attention
+    // workspaces for the rounded context
+    const int ws_ctx = (cfg->max_ctx + 255) / 256 * 256;
+    E.attn_ws = (float*)E.dalloc<char>(std::max(attn_decode_workspace_bytes(cfg->max_batch, E.Hq, ws_ctx),
+                                                attn_decode2_workspace_bytes(cfg->max_batch, E.Hq, ws_ctx,
                                                                              E.attn_ppb)),
                                        true);
     E.slabs = E.dalloc<float>((size_t)ms_engine::kMaxSplit * std::min(std::max(cfg->max_batch, 64), 256) *
@@ -888,9 +863,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.attn_ppw = attn_decode_ppw(cfg->max_batch, E.Hk, cfg->max_ctx);
     if (const char* v = getenv("MS_QSPLIT")) E.qsplit = atoi(v);
     if (const char* v = getenv("MS_RESID_FUSED")) E.resid_fuse = atoi(v) != 0;
-    if (const char* v = getenv("MS_MLP_FUSED")) E.mlp_fuse = atoi(v) != 0;
     if (const char* v = getenv("MS_DECODE_TAIL")) E.tail_fuse = atoi(v) != 0;
-    if (const char* v = getenv("MS_QKV_ATTN")) E.qkv_attn = atoi(v) != 0;
     if (const char* v = getenv("MS_QRESID")) E.qresid = atoi(v) != 0;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_rt = 16;
     if (E.H % E.resid_rt || E.H / E.resid_rt > 256) E.resid_fuse = false;
@@ -914,9 +887,23 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     HIP_OK(hipHostMalloc((void**)&E.ids_host, (size_t)ms_engine::kMaxRun * 256 * sizeof(int32_t),
                          hipHostMallocDefault));
     E.ids_ring_d = E.dalloc<int32_t>((size_t)ms_engine::kMaxRun * 256);
-    E.mlp_sync_d = E.dalloc<unsigned>(64, true);
-    HIP_OK(hipHostMalloc((void**)&E.mlp_err_h, 64, hipHostMallocDefault));
-    *E.mlp_err_h = 0;
+    // the persistent decode step (k_persist.hip)
+    {
+      int dev_cu = 0;
+      HIP_OK(hipDeviceGetAttribute(&dev_cu, hipDeviceAttributeMultiprocessorCount, cfg->device));
+      E.n_cu = dev_cu;
+      if (const char* v = getenv("MS_PERSIST")) E.persist = atoi(v) != 0;
+      const int np_ws = (ws_ctx + kPage - 1) / kPage;
+      E.nsplit_ws = (np_ws + E.attn_ppb - 1) / E.attn_ppb;
+      E.persist_ok = persist_supported(cfg->max_batch, E.H, E.F, E.Hq, E.Hk, E.D, E.L, E.attn_ppb, E.n_cu) &&
+                     E.slot_major && E.attn_v2 && E.resid_rt == 12;
+      E.pk_sync = E.dalloc<unsigned>(persist_sync_words(E.L), true);
+      E.pk_err_d = E.dalloc<unsigned>(4, true);
+      HIP_OK(hipHostMalloc((void**)&E.pk_err_h, 64, hipHostMallocDefault));
+      *E.pk_err_h = 0;
+      E.pk_xg2 = E.dalloc<f16_t>((size_t)cfg->max_batch * E.H);
+      E.pk_ssq2 = E.dalloc<float>((size_t)256 * cfg->max_batch, true);
+    }
     HIP_OK(hipHostMalloc((void**)&E.first_host, (size_t)cfg->max_batch * sizeof(int32_t), hipHostMallocDefault));
     if (const char* v = getenv("MS_DECODE_RUN")) E.max_run = std::max(1, std::min(atoi(v), (int)ms_engine::kMaxRun));
     if (const char* ng = getenv("MAPSUM_NO_GRAPHS")) E.use_graphs = !(ng[0] == '1');
@@ -940,7 +927,7 @@ int ms_destroy(ms_engine* e) {
   for (ms_engine::Ctx* c : {&e->cp, &e->cd})
     if (c->args_h) (void)hipHostFree(c->args_h);
   if (e->ids_host) (void)hipHostFree(e->ids_host);
-  if (e->mlp_err_h) (void)hipHostFree(e->mlp_err_h);
+  if (e->pk_err_h) (void)hipHostFree(e->pk_err_h);
   if (e->first_host) (void)hipHostFree(e->first_host);
   if (e->bt_h) (void)hipHostFree(e->bt_h);
   for (auto& kv : e->decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
@@ -1455,6 +1442,48 @@ static void decode_tail(ms_engine& E, int B, int32_t* d, int tiles) {
   decode_head(E, B, d);
 }
 
+// every layer of one decode step as the persistent launch (k_persist.hip): enters with layer 0's
+// input in x / xb / ssq (one-tile statistics) and leaves the final norm's input in xb / ssq with
+// 256 statistics tiles, like the per-layer launches it replaces
+static void persist_layers(ms_engine& E, int B, const DecodeAttnArgs& da) {
+  PkArgs a{};
+  for (int l = 0; l < E.L; ++l) {
+    const Layer& Ly = E.layers[l];
+    const KVView kv = E.kv_layer(l);
+    a.layers[l] = PkLayer{Ly.wqkv, Ly.wo, Ly.wgu, Ly.wdown, Ly.ffn_norm,
+                          l + 1 < E.L ? E.layers[l + 1].attn_norm : E.final_norm, kv.k, kv.v};
+  }
+  a.L = E.L;
+  a.B = B;
+  a.seq_len = da.seq_len;
+  a.seq_slot = da.seq_slot;
+  a.max_pages = E.max_pages;
+  a.ppb = E.attn_ppb;
+  a.nsplit_ws = E.nsplit_ws;
+  a.cos_tab = E.cos_tab;
+  a.sin_tab = E.sin_tab;
+  a.eps = E.cfg.norm_eps;
+  a.inv_h = 1.0f / (float)E.H;
+  a.scale_log2 = 1.4426950408889634f / sqrtf((float)E.D);
+  a.rs0_tiles = E.cur_rs.tiles;
+  a.x = E.x;
+  a.xb = E.xb;
+  a.ssq = E.ssq;
+  a.slabs = E.slabs;
+  a.ws = E.attn_ws;
+  a.attn = E.attn;
+  a.xg2 = E.pk_xg2;
+  a.ssq2 = E.pk_ssq2;
+  a.hbuf = E.hbuf;
+  a.sync = E.pk_sync;
+  a.err = E.pk_err_d;
+  E.prof_begin(K_PERSIST);
+  launch_decode_step(a, E.stream);
+  E.prof_end(K_PERSIST);
+  E.pending_split = 0;
+  E.cur_rs = make_row_scale(E.ssq, E.H / E.resid_rt, E.H, E.cfg.norm_eps);
+}
+
 // kernels of one decode step (no host synchronisation: capturable into a hipGraph).  Enters
 // with the step's layer-0 input in x / xb / ssq and leaves the NEXT step's there: the greedy
 // ids, the argument advance and the next embedding gather are one launch (decode_tail_kernel)
@@ -1464,8 +1493,12 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
   PrefillAttnArgs pa{};
   E.pending_split = 0;
   E.cur_rs = E.norm_rs();
-  // every layer leaves xb = f16(x * the next gain) with its deferred scale in cur_rs
-  for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
+  if (E.persist_on(B)) {
+    persist_layers(E, B, da);
+  } else {
+    // every layer leaves xb = f16(x * the next gain) with its deferred scale in cur_rs
+    for (int l = 0; l < E.L; ++l) E.run_layer(l, B, true, d + o_pos, d + o_slot, pa, da);
+  }
   const RowScale rs = E.cur_rs;
   if (E.large(B) && dgemm_supported(B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX, 1)) {
     const int tiles = E.V / 16;
@@ -1514,6 +1547,9 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   for (Seq* s : batch) { a.push_back(s->len + 1); max_len = std::max(max_len, s->len + 1); }
   a.push_back(0);                                   // [4B]     step of the run (ring row)
   a.push_back(0);                                   // [4B+1]   decode_tail's arrival ticket
+  // the persistent step runs (captured or eagerly) exactly when persist_on holds for this run;
+  // toggling it drops the cached graphs (ms_set_persist, the timeout fallback below)
+  E.pk_used = E.persist_on(B);
   HIP_OK(hipEventRecord(E.ev_a, E.stream));
   int32_t* d = E.upload_args(a);
   decode_head(E, B, d);  // the first step's input; each step's tail gathers the next one's
@@ -1553,25 +1589,31 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   HIP_OK(hipEventRecord(E.ev_b, E.stream));
   HIP_OK(hipMemcpyAsync(E.ids_host, E.ids_ring_d, (size_t)k * B * sizeof(int32_t), hipMemcpyDeviceToHost,
                         E.stream));
-  if (E.mlp_used || E.qa_used)
-    HIP_OK(hipMemcpyAsync(E.mlp_err_h, E.mlp_sync_d + 16, sizeof(unsigned), hipMemcpyDeviceToHost, E.stream));
+  if (E.pk_used)
+    HIP_OK(hipMemcpyAsync(E.pk_err_h, E.pk_err_d, sizeof(unsigned), hipMemcpyDeviceToHost, E.stream));
   ids.resize((size_t)k * B);
   HIP_OK(hipStreamSynchronize(E.stream));
-  if ((E.mlp_used || E.qa_used) && *E.mlp_err_h) {  // a workgroup of a fused launch was not resident: never silent
-    // fall back to the two launches for good: clear the device flag and the counters, and drop
-    // every captured graph that still holds mlp_decode_kernel; the run's ids are discarded (the
-    // sequences did not advance), so the next ms_step recomputes them unfused
-    E.mlp_fuse = false;
-    E.mlp_used = false;
-    E.qkv_attn = false;
-    E.qa_used = false;
-    HIP_OK(hipMemsetAsync(E.mlp_sync_d, 0, 64 * sizeof(unsigned), E.stream));
+  if (E.pk_used && *E.pk_err_h) {
+    // a hand-off of the persistent step timed out (a workgroup was not resident): never silent,
+    // never a hang.  Turn the persistent step off for this engine, reset its counters and flag,
+    // drop every graph that holds it, and recompute the whole run with the per-layer launches:
+    // the run started from the sequences' own state (args above), and every K / V row it wrote
+    // is at a position the recomputation writes again
+    fprintf(stderr, "mapsum: persistent decode step timed out (code 0x%x); recomputing with the launches\n",
+            *E.pk_err_h);
+    E.persist = false;
+    E.pk_used = false;
+    HIP_OK(hipMemsetAsync(E.pk_sync, 0, persist_sync_words(E.L) * sizeof(unsigned), E.stream));
+    HIP_OK(hipMemsetAsync(E.pk_err_d, 0, 4 * sizeof(unsigned), E.stream));
     HIP_OK(hipStreamSynchronize(E.stream));
-    *E.mlp_err_h = 0;
+    *E.pk_err_h = 0;
     E.drop_graphs();
-    REQUIRE(false, MS_EIO, "fused decode launch (MLP / QKV + attention): hand-off timed out (not every "
-                           "workgroup resident); fusion disabled for this engine, the run's ids were discarded");
+    E.stats.persist_fallbacks += 1;
+    decode_run(E, batch, k, ids);
+    return;
   }
+  if (E.pk_used) E.stats.persist_steps += k;
+  E.pk_used = false;
   std::memcpy(ids.data(), E.ids_host, (size_t)k * B * sizeof(int32_t));
 }
 
@@ -1736,9 +1778,40 @@ int ms_set_profiling(ms_engine* e, uint32_t mask) {
   return MS_OK;
 }
 
-int ms_debug_qa_stamps(uint64_t* out, int32_t n) {
+int ms_set_persist(ms_engine* e, int32_t on) {
+  if (!e) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    HIP_OK(hipStreamSynchronize(e->cd.stream));
+    e->persist = on != 0;
+    e->drop_graphs();
+    return (e->persist_ok ? 1 : 0);
+  });
+}
+
+int ms_debug_read(ms_engine* e, int32_t which, int64_t offset, void* host, int64_t bytes) {
+  if (!e || !host || offset < 0 || bytes < 0) return MS_EINVAL;
+  return guarded(e, [&]() -> int {
+    ms_engine& E = *e;
+    const void* base = nullptr;
+    size_t cap = 0;
+    switch (which) {
+      case MS_DBG_KPOOL: base = E.kpool; cap = E.layer_kv_elems * E.L * sizeof(f16_t); break;
+      case MS_DBG_VPOOL: base = E.vpool; cap = E.layer_kv_elems * E.L * sizeof(f16_t); break;
+      case MS_DBG_DECODE_LOGITS: base = E.cd.logits; cap = (size_t)E.cfg.max_batch * E.V * sizeof(float); break;
+      case MS_DBG_DECODE_X: base = E.cd.x; cap = (size_t)E.cfg.max_batch * E.H * sizeof(float); break;
+      default: REQUIRE(false, MS_EINVAL, "ms_debug_read: unknown buffer");
+    }
+    REQUIRE((size_t)offset + (size_t)bytes <= cap, MS_EINVAL, "ms_debug_read: range past the buffer");
+    HIP_OK(hipStreamSynchronize(E.cd.stream));
+    HIP_OK(hipStreamSynchronize(E.cp.stream));
+    HIP_OK(hipMemcpy(host, (const char*)base + offset, (size_t)bytes, hipMemcpyDeviceToHost));
+    return MS_OK;
+  });
+}
+
+int ms_debug_pk_stamps(uint64_t* out, int32_t n) {
   if (!out || n < 0) return MS_EINVAL;
-  ms::qkv_attn_stamps(reinterpret_cast<unsigned long long*>(out), n);
+  ms::persist_stamps(reinterpret_cast<unsigned long long*>(out), n);
   return MS_OK;
 }
 

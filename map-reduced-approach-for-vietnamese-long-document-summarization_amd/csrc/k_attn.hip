@@ -679,10 +679,9 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
 // XCD-matched grid (placement only) and the v2 prologue form (3: the prologue wave); both give
 // the same bits.  Read at launch: a captured decode graph keeps what it was captured with.
 static int g_combine_grp = [] { const char* e = getenv("MS_COMBINE_GRP"); return e ? atoi(e) : 1; }();
-static int g_a2_order = [] { const char* e = getenv("MS_A2_ORDER"); return e ? atoi(e) : 0; }();
 void set_attn_tuning(int combine_grp, int order) {
+  (void)order;  // the v2 prologue-wave form (order 3) was removed in round 6: one form remains
   g_combine_grp = combine_grp;
-  g_a2_order = order;
 }
 static bool combine_grp_ok(int B, int Hk) { return g_combine_grp != 0 && (B * Hk) % 8 == 0; }
 
@@ -748,7 +747,6 @@ namespace ms {
 // wave order; the block writes the split's partial (attn_decode_combine_kernel merges them in
 // split order) or, with a single split, the fp16 output itself.  Arithmetic per page is the
 // kernel above's (same MFMA orientation, fp16 P, lazy-free online softmax per page).
-constexpr int kPwElems = 10;  // prologue elements per lane of the prologue wave: (G + 2) * 128 / 64
 constexpr int kPpbMin = 4, kPpbMax = 9;  // 9 x 16 KB V images + the prologue fit 160 KB of LDS
 
 int attn_decode2_ppb(int max_batch, int Hk, int max_ctx) {
@@ -764,9 +762,6 @@ static size_t attn2_lds_bytes(int ppb, int G) {
   // + 16 B: the prologue wave's flag (PW)
   return (size_t)ppb * 16384 + (size_t)(G + 2) * kHeadDim * 4 + (size_t)(G + 2) * kHeadDim * 2 + 16;
 }
-// the prologue-wave form (PW) fits: its 64 lanes hold the G + 2 fold vectors, <= kPwElems each
-static bool attn2_pw_ok(int G) { return (G + 2) * kHeadDim <= 64 * kPwElems; }
-
 bool attn_decode2_supported(int B, int Hq, int Hk, int max_len, int ppb) {
   (void)B;
   if (Hk < 1 || Hq % Hk || Hq / Hk > kMaxGroup || ppb < kPpbMin || ppb > kPpbMax) return false;
@@ -798,27 +793,12 @@ __device__ unsigned long long g_a2_stamps[kA2StampBlocks * kA2Stamps];
       stamps[blockIdx.x * kA2Stamps + (k)] = __builtin_amdgcn_s_memrealtime();                    \
   } while (0)
 
-// PW: one more wave per block, the PROLOGUE wave (wave PPB, no page): the prologue operands are
-// fetched and folded by it alone while the PPB page waves issue their pages at once.  A CU's
-// vector memory instructions are accepted and served in issue order across its waves (its queue
-// holds roughly the block's page loads): in the all-waves prologue (PW = false) the later waves
-// could not even ISSUE their prologue loads until the earlier waves' pages had drained, and
-// since every S waits for the block-wide prologue, no wave computed before ~12 of the block's
-// ~15.5 us (stamps, profiles/r05/v12_*).  Here the prologue wave issues its ~60 loads first
-// (every page wave waits at one barrier for that), folds them, rotates q / k, writes the new
-// token's K / V and raises an LDS flag; each page wave polls the flag (LDS only) once its K has
-// landed, so the waves' S / P.V run as their pages arrive.  Same arithmetic, same bits
-// (attn2_pw_ok: G + 2 vectors of 128 over the wave's 64 lanes, <= 10 per lane).  Opt-in
-// (MS_A2_ORDER=3), measured no faster: even at the head of the CU's queue the ~60 prologue loads
-// take ~6.5 us (first S at 8.7 instead of 12.7 us), and the block still ends ~2 us after its
-// last page lands (~13.5 us): the launch is bound by its page stream, not by the prologue.
-template <bool FROM_SLABS, int PPB, bool TICKET, bool PW = false>
-__global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel(
+template <bool FROM_SLABS, int PPB, bool TICKET>
+__global__ __launch_bounds__(64 * PPB) void attn_decode2_kernel(
     DecodeQKV qa, int Hq, int Hk, KVView kv, DecodeAttnArgs a, float* __restrict__ ws, f16_t* __restrict__ out,
     int nsplit, float scale_log2, unsigned* __restrict__ cnt, unsigned long long* __restrict__ stamps) {
-  static_assert(!PW || (FROM_SLABS && !TICKET), "the prologue wave folds the QKV slabs, no ticket merge");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int NTHR = 64 * (PPB + (PW ? 1 : 0));
+  constexpr int NTHR = 64 * PPB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -829,7 +809,6 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
   const int len = a.seq_len[b];
   const int slot = a.seq_slot[b];
   const int np = (len + kPage - 1) / kPage;
-  const bool pro = PW && wave == PPB;  // the prologue wave (wave-uniform)
   const int pg = split * PPB + wave;  // this wave's page (none when >= np)
   const int pos = len - 1;            // the new token
   const int row_stride = (Hq + 2 * Hk) * kHeadDim;
@@ -838,8 +817,7 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
   f16_t* qn = (f16_t*)(raw + (G + 2) * kHeadDim);     // [G][128] roped q
   f16_t* kn = qn + G * kHeadDim;                       // [128] roped k of the new token
   f16_t* vn = kn + kHeadDim;                           // [128] v of the new token
-  volatile unsigned* pw_flag = (volatile unsigned*)(vn + kHeadDim);  // PW: prologue published
-  const bool has_page = !pro && pg < np;               // wave-uniform
+  const bool has_page = pg < np;                       // wave-uniform
   if (wave == PPB - 1) A2_STAMP(24);
   if (stamps && wave == 0) {
     A2_STAMP(0);
@@ -860,38 +838,7 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
   float rv[4] = {0.f, 0.f, 0.f, 0.f};
   float sv[PER][kMaxSlabs];
   float rcs = 0.f, rsn = 0.f;
-  float pv[PW ? kPwElems : 1][PW ? kMaxSlabs : 1];
-  if constexpr (PW) {
-    if (pro) {
-      *pw_flag = 0u;
-      if (qa.rs.ssq) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int t = lane + 64 * i;
-          if (64 * i < qa.rs.tiles) rv[i] = ld_f32_opaque(qa.rs.ssq + (size_t)min(t, qa.rs.tiles - 1) * a.B + b);
-        }
-      }
-      const size_t sstride = (size_t)a.B * row_stride;
-      const float* src = qa.slabs + (size_t)b * row_stride;
-#pragma unroll
-      for (int i = 0; i < kPwElems; ++i) {
-        if (64 * i < nvec) {  // wave-uniform
-          const int e = min(lane + 64 * i, nvec - 1);
-          const int hh = e >> 7, j = e & 127;
-          const int col = hh < G ? (kvh * G + hh) * kHeadDim + j
-                                 : (hh == G ? (Hq + kvh) * kHeadDim + j : (Hq + Hk + kvh) * kHeadDim + j);
-#pragma unroll
-          for (int q = 0; q < kMaxSlabs; ++q)
-            if (q < qa.S) pv[i][q] = ld_f32_opaque(src + q * sstride + col);
-        }
-      }
-      rcs = ld_f32_opaque(qa.cos_tab + (size_t)pos * 64 + lane);
-      rsn = ld_f32_opaque(qa.sin_tab + (size_t)pos * 64 + lane);
-      A2_STAMP(26);
-    }
-    // every page wave issues its page only after the prologue wave's loads are queued
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  } else if constexpr (FROM_SLABS) {
+  if constexpr (FROM_SLABS) {
     if (qa.rs.ssq) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -938,64 +885,7 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
 
   // 2. prologue: fold the slabs, the row scale, RoPE -> qn / kn / vn; the owner writes the new
   // token's K/V into the cache (rope_kv_kernel's arithmetic, as the kernel above)
-  if constexpr (PW) {
-    if (pro) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(rv[i]));
-#pragma unroll
-      for (int i = 0; i < kPwElems; ++i)
-#pragma unroll
-        for (int q = 0; q < kMaxSlabs; ++q) asm volatile("" : "+v"(pv[i][q]));
-      asm volatile("" : "+v"(rcs), "+v"(rsn));
-      float rsum = 0.f;
-      if (qa.rs.ssq) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (!(lane + 64 * i < qa.rs.tiles)) rv[i] = 0.f;
-        rsum = ((rv[0] + rv[1]) + rv[2]) + rv[3];
-      }
-      const float rrow = qa.rs.ssq ? rs_rinv(wave_sum(rsum), qa.rs) : 1.0f;
-#pragma unroll
-      for (int i = 0; i < kPwElems; ++i) {
-        const int e = lane + 64 * i;
-        if (64 * i >= nvec) break;
-        float acc = pv[i][0];
-#pragma unroll
-        for (int q = 1; q < kMaxSlabs; ++q)
-          if (q < qa.S) acc += pv[i][q];
-        if (e < nvec) raw[e] = h2f(f2h(acc * rrow));
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): raw is in LDS for the whole wave
-      __builtin_amdgcn_wave_barrier();
-      const int nh = G + (owns_new ? 1 : 0);  // (head, i) pairs: the q heads, then k; i = lane
-      for (int hh = 0; hh < nh; ++hh) {
-        const float lo = raw[hh * kHeadDim + rope_perm(lane)], hi = raw[hh * kHeadDim + rope_perm(64 + lane)];
-        const float ra = __fsub_rn(__fmul_rn(lo, rcs), __fmul_rn(hi, rsn));
-        const float rb = __fadd_rn(__fmul_rn(hi, rcs), __fmul_rn(lo, rsn));
-        f16_t* dst = hh < G ? qn + hh * kHeadDim : kn;
-        dst[lane] = f2h(ra);
-        dst[64 + lane] = f2h(rb);
-      }
-      if (owns_new) {
-        vn[lane] = f2h(raw[(G + 1) * kHeadDim + lane]);
-        vn[64 + lane] = f2h(raw[(G + 1) * kHeadDim + 64 + lane]);
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      __builtin_amdgcn_wave_barrier();
-      if (owns_new) {
-        const size_t o0 = (((size_t)slot * kv.max_pages + pos / kPage) * kv.n_kv_heads + kvh) * kPage + pos % kPage;
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          const size_t o = o0 * kHeadDim + lane + 64 * h2;
-          kv.k[o] = kn[lane + 64 * h2];
-          kv.v[o] = vn[lane + 64 * h2];
-        }
-      }
-      *pw_flag = 1u;  // after the wave's qn / kn / vn writes (one wave's LDS ops complete in order)
-      A2_STAMP(2);
-    }
-  } else if constexpr (FROM_SLABS) {
+  if constexpr (FROM_SLABS) {
     // the opaque loads above have landed once at most the page's 32 are in flight
     if (has_page) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1046,7 +936,7 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
       kv.v[o] = vn[tid];
     }
   }
-  if (!PW && wave == 0) A2_STAMP(2);
+  if (wave == 0) A2_STAMP(2);
 
   // 3. S^T = K Q^T, softmax over the page, O^T = V^T P^T
   f32x4 o[8];
@@ -1056,13 +946,6 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
   if (has_page) {
     f16x8 qf[4];
     const int hl = min(r, G - 1);
-    if constexpr (PW) {
-      // the page's K has landed (its loads are older than the poll's), then wait for the prologue
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      // (bounded: the prologue wave always raises the flag; a bound turns a bug into wrong
-      // numbers the tests catch instead of a hung GPU)
-      for (int it = 0; *pw_flag == 0u && it < (1 << 22); ++it) __builtin_amdgcn_s_sleep(1);
-    }
     if constexpr (FROM_SLABS) {
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) qf[s4] = *(const f16x8*)(qn + hl * kHeadDim + 32 * s4 + 8 * g);
@@ -1135,7 +1018,7 @@ __global__ __launch_bounds__(64 * (PPB + (PW ? 1 : 0))) void attn_decode2_kernel
     A2_STAMP(12 + wave);
   }
   // 4. publish (m, l, O^T) of this wave's 16 columns into its own LDS region, merge in wave order
-  if (!pro) {
+  {
     float* mw = (float*)vs_;
     if (g == 0) { mw[r * 130 + 0] = m_run; mw[r * 130 + 1] = l_run; }
 #pragma unroll
@@ -1218,10 +1101,6 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
   const float scale_log2 = kLog2e / sqrtf((float)kHeadDim);
   const dim3 grid(a.B * Hk * nsplit);
   const size_t lds = attn2_lds_bytes(ppb, Hq / Hk);
-  // order 3: the prologue-wave form (PW; opt-in -- bit-identical, measured no faster: the first
-  // S moves from 12.7 to 8.7 us into the block, but the block still ends when its last page
-  // lands, 18.84 vs 18.72 us per launch, decode 2.109 vs 2.105 ms per step, profiles/r05/v12_*)
-  const bool pw = g_a2_order == 3 && qa.slabs && !cnt && attn2_pw_ok(Hq / Hk);
   static unsigned long long* stamps = [] {
     const char* e = getenv("MS_A2_STAMPS");
     void* p = nullptr;
@@ -1233,9 +1112,6 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
     if (qa.slabs && cnt)                                                                                      \
       MS_LAUNCH((attn_decode2_kernel<true, P_, true>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,    \
                 out, nsplit, scale_log2, cnt, stamps);                                                        \
-    else if (qa.slabs && pw)                                                                                  \
-      MS_LAUNCH((attn_decode2_kernel<true, P_, false, true>), grid, dim3(64 * (P_ + 1)), lds, s, qa, Hq, Hk,  \
-                kv, a, ws, out, nsplit, scale_log2, cnt, stamps);                                             \
     else if (qa.slabs)                                                                                        \
       MS_LAUNCH((attn_decode2_kernel<true, P_, false>), grid, dim3(64 * P_), lds, s, qa, Hq, Hk, kv, a, ws,   \
                 out, nsplit, scale_log2, cnt, stamps);                                                        \

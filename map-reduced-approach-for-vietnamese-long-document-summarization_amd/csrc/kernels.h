@@ -123,8 +123,8 @@ void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K,
 void set_gemm_variant(int v);
 // the Q6_K lm_head argmax GEMV: grid-stride two-stage loop (default) or one-tile blocks
 void set_qgemv_gs(bool on);
-// decode attention: the combine's XCD-matched grid (1, default) and the v2 prologue form
-// (0 default, 3 the prologue wave) -- placement / schedule only, the same bits
+// decode attention: the combine's XCD-matched grid (1, default) or the (B, Hq) grid (0) --
+// placement only, the same bits (order: 0; the prologue-wave form was removed in round 6)
 void set_attn_tuning(int combine_grp, int order);
 // large-batch skinny GEMM: 1 = 4-wave blocks, 2 = 8-wave blocks with the K step split in halves
 // (S = 1 launches; a different but M-independent sum order)
@@ -171,14 +171,6 @@ struct GemvArgs {
   // writes its rows into the batch's [S][B][N] slabs (slab_rows = B, out = slab 0, row r0)
   int slab_rows;
 };
-// the decode MLP of one layer as one launch (k_mlp.hip): h = SwiGLU(rs . xb Wgu^T) [M][F], then
-// x += h Wdown^T with the RESID_SSQ epilogue on 12-row tiles (ssq_out [256][M], xg_out =
-// f16(x * gamma_next)); bit-identical to the two GEMV launches.  sync: 2 zeroed counters the
-// kernel leaves zeroed; err: set on a hand-off timeout.  M <= 8, H = 3072, F = 8192.
-bool mlp_decode_supported(int M, int H, int F, int rs_tiles);
-void launch_mlp_decode(const f16_t* xb, const f16_t* wgu, const f16_t* wdown, f16_t* h, float* x, int M, int H,
-                       int F, const RowScale& rs, float* ssq_out, const f16_t* gamma_next, f16_t* xg_out,
-                       unsigned* sync, unsigned* err, hipStream_t s);
 // split-K into S fp32 slabs [S][M][N] (slab s = partial over k in [s*K/S, (s+1)*K/S)); the
 // consumer adds them in slab order (launch_residual_rmsnorm / the decode attention prologue)
 bool gemv_split_supported(int M, int N, int K, int S, int rs_tiles = 0);
@@ -292,20 +284,52 @@ void launch_attn_decode2(const DecodeQKV& qa, f16_t* out, int Hq, int Hk, KVView
 // merge nsplit decode-attention partials (launch_attn_decode2's workspace layout) into out
 void launch_attn_combine(const float* ws, f16_t* out, int B, int Hq, int Hk, int nsplit, hipStream_t s);
 
-// The decode step's QKV projection and attention as ONE launch (k_qkvattn.hip): 256 workgroups
-// (one per CU, all resident) each compute 20 rows of the QKV projection -- bit-identical to the
-// split-6 GEMV + slab fold -- publish them (write-through) to qkv32 [B][QKVN] behind a per-kv-head
-// arrival counter, and run one (sequence, kv head, split) item of launch_attn_decode2 (ppb page
-// waves) whose K/V pages are already in flight.  sync: >= 32 zeroed words the kernel leaves zeroed;
-// err: set when a hand-off wait gives up (a workgroup was not resident) -- never a hang.
-bool qkv_attn_supported(int B, int max_batch, int H, int Hq, int Hk, int max_len, int ppb, int split_qkv);
-// diagnostic: the latest launch's phase stamps [256][16] (MS_QA_STAMPS=1), 100 MHz ticks
-void qkv_attn_stamps(unsigned long long* host, int n);
 // decode attention v2's per-block phase stamps of its latest launch (MS_A2_STAMPS=1), [1024][32]
 void attn2_stamps(unsigned long long* host, int n);
-void launch_qkv_attn(const f16_t* xb, const f16_t* wqkv, float* qkv32, const DecodeQKV& qa, f16_t* out, int Hq,
-                     int Hk, KVView kv, DecodeAttnArgs a, float* ws, int ppb, unsigned* sync, unsigned* err,
-                     hipStream_t s);
+
+// ---- the decode step's layers as ONE persistent launch (k_persist.hip): engines of <= 8 slots
+// on fp16 Llama-3.2-3B weights (persist_supported), bit-identical to the per-layer launches
+struct PkLayer {
+  const f16_t* wqkv;
+  const f16_t* wo;
+  const f16_t* wgu;
+  const f16_t* wdown;
+  const f16_t* ffn_norm;
+  const f16_t* g_next;  // the next layer's attn_norm, or the final norm
+  f16_t* kc;            // this layer's K / V pools (slot-major pages)
+  f16_t* vc;
+};
+
+struct PkArgs {
+  PkLayer layers[28];  // kernel arguments: scalar loads, nothing queued behind the loader's DMA
+  int L, B;
+  const int32_t* seq_len;   // [B] keys incl. the new token
+  const int32_t* seq_slot;  // [B]
+  int max_pages, ppb, nsplit_ws;
+  const float* cos_tab;
+  const float* sin_tab;
+  float eps, inv_h, scale_log2;
+  int rs0_tiles;  // statistics tiles behind layer 0's xb (1: the embedding kernel)
+  float* x;       // [B][H] residual
+  f16_t* xb;      // [B][H] QKV input; the down epilogue writes the next one
+  float* ssq;     // [tiles][B]
+  float* slabs;   // [6][B][QKVN]
+  float* ws;      // attention split partials [B][HQ][nsplit_ws][132]
+  f16_t* attn;    // [B][H]
+  f16_t* xg2;     // [B][H] gate/up input
+  float* ssq2;    // [256][B]
+  f16_t* hbuf;    // [B][F]
+  unsigned* sync;  // [L * SL + 1] counters (zero between launches: the last workgroup resets them)
+  unsigned* err;   // set on a hand-off timeout (never cleared here)
+  unsigned spin;   // global polls before a hand-off gives up (MS_PK_SPIN; tests force 0)
+  unsigned long long* stamps;  // diagnostic timeline (MS_PK_STAMPS=1): [256][L][16] s_memrealtime
+};
+// the persistent step's in-kernel timeline of its latest launch (MS_PK_STAMPS=1), [256][L][16]
+void persist_stamps(unsigned long long* host, int n);
+
+size_t persist_sync_words(int L);
+bool persist_supported(int max_batch, int H, int F, int Hq, int Hk, int Dh, int L, int ppb, int n_cu);
+void launch_decode_step(const PkArgs& a, hipStream_t s);
 
 // synthetic weights (oracle/synth.py restates this generator)
 // row maps: dst_row = (r >> 4) * map_mul + (r & 15) + map_add, or with map_mul == 0 the

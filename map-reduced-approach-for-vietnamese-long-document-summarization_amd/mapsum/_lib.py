@@ -25,7 +25,8 @@ MS_EPI_ARGMAX = 5
 GEMM_DEFAULT = 4
 MS_GGML_Q4_K, MS_GGML_Q6_K = 12, 14
 # kernel classes of ms_stats.kernel_ms
-K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC, K_QKV_ATTN = range(7)
+K_GEMM, K_ATTN_PREFILL, K_GEMV, K_ATTN_DECODE, K_LMHEAD, K_MISC, K_PERSIST = range(7)
+MS_DBG_KPOOL, MS_DBG_VPOOL, MS_DBG_DECODE_LOGITS, MS_DBG_DECODE_X = range(4)
 
 EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
@@ -37,7 +38,7 @@ EXPORTED = (
     "ms_weight_regions", "ms_quant_manifest", "ms_declare_weight_q",
     "ms_forward_packed", "ms_submit_forced", "ms_set_eos_ids", "ms_op_gemv_strided",
     "ms_op_gemv_resid", "ms_op_set_row_scale", "ms_op_gemm_resid", "ms_gemm_resid_tiles",
-    "ms_trace_push", "ms_trace_pop", "ms_debug_qa_stamps", "ms_debug_a2_stamps",
+    "ms_trace_push", "ms_trace_pop", "ms_debug_a2_stamps", "ms_set_persist", "ms_debug_read", "ms_debug_pk_stamps",
 )
 
 
@@ -64,7 +65,8 @@ class MsStats(C.Structure):
                 ("prefill_passes", C.c_int64), ("decode_steps", C.c_int64), ("finished", C.c_int64),
                 ("prefill_ms", C.c_double), ("decode_ms", C.c_double),
                 ("kernel_ms", C.c_double * 8), ("kernel_launches", C.c_int64 * 8),
-                ("decode_kv_tokens", C.c_int64), ("graphs_built", C.c_int64)]
+                ("decode_kv_tokens", C.c_int64), ("graphs_built", C.c_int64),
+                ("persist_fallbacks", C.c_int64), ("persist_steps", C.c_int64)]
 
 
 _lib = None
@@ -137,7 +139,9 @@ def load_at(path: str, ab: bool = True) -> C.CDLL:
         "ms_declare_weight_q": (i32, [vp, i32, i32, i32]),
         "ms_trace_push": (i32, [C.c_char_p]),
         "ms_trace_pop": (i32, []),
-        "ms_debug_qa_stamps": (i32, [vp, i32]),
+        "ms_set_persist": (i32, [vp, i32]),
+        "ms_debug_read": (i32, [vp, i32, i64, vp, i64]),
+        "ms_debug_pk_stamps": (i32, [vp, i32]),
         "ms_debug_a2_stamps": (i32, [vp, i32]),
     }
     for name, (res, args) in sig.items():

@@ -50,6 +50,28 @@ class ModelConfig:
         return 2 * self.n_layers * self.n_kv_heads * self.head_dim * 2
 
 
+def llama3_rope_factors(cfg):
+    """The per-frequency divisors of llama3 RoPE scaling, float64 [head_dim / 2]: base inverse
+    frequency / scaled one -- what llama.cpp's converter stores as the GGUF ``rope_freqs.weight``
+    tensor and what the engine's own cos / sin tables apply (engine.cpp rope_tables).  All ones
+    without scaling (rope_factor 0)."""
+    import math
+
+    import numpy as np
+    D = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (np.arange(0, D, 2, dtype=np.float64) / D))
+    if not cfg.rope_factor or cfg.rope_factor <= 0:
+        return np.ones_like(inv)
+    low_wl = cfg.rope_orig_ctx / cfg.rope_low_freq_factor
+    high_wl = cfg.rope_orig_ctx / cfg.rope_high_freq_factor
+    wl = 2.0 * math.pi / inv
+    out = np.where(wl > low_wl, inv / cfg.rope_factor, inv)
+    smooth = (cfg.rope_orig_ctx / wl - cfg.rope_low_freq_factor) / (cfg.rope_high_freq_factor - cfg.rope_low_freq_factor)
+    smoothed = (1.0 - smooth) * out / cfg.rope_factor + smooth * out
+    medium = ~(wl < high_wl) & ~(wl > low_wl)
+    return inv / np.where(medium, smoothed, out)
+
+
 LLAMA32_3B = ModelConfig(name="llama3.2-3b", n_layers=28, hidden=3072, n_heads=24, n_kv_heads=8,
                          head_dim=128, ffn=8192, vocab=128256)
 

@@ -282,4 +282,16 @@ class Engine(RequestQueue):
                 "prefill_passes": s.prefill_passes, "decode_steps": s.decode_steps,
                 "finished": s.finished, "prefill_ms": s.prefill_ms, "decode_ms": s.decode_ms,
                 "kernel_ms": list(s.kernel_ms), "kernel_launches": list(s.kernel_launches),
-                "decode_kv_tokens": s.decode_kv_tokens, "graphs_built": s.graphs_built}
+                "decode_kv_tokens": s.decode_kv_tokens, "graphs_built": s.graphs_built,
+                "persist_fallbacks": s.persist_fallbacks, "persist_steps": s.persist_steps}
+
+    def set_persist(self, on: bool) -> bool:
+        """The decode step's layers as one persistent launch (k_persist.hip) or the per-layer
+        launches; returns whether this engine supports the persistent step at all."""
+        return bool(self._chk(self.lib.ms_set_persist(self.h, 1 if on else 0), "ms_set_persist"))
+
+    def debug_read(self, which: int, offset: int, nbytes: int) -> np.ndarray:
+        """Test hook: `nbytes` of an engine buffer (L.MS_DBG_*) from byte `offset`, as uint8."""
+        out = np.empty(nbytes, np.uint8)
+        self._chk(self.lib.ms_debug_read(self.h, which, offset, out.ctypes.data, nbytes), "ms_debug_read")
+        return out

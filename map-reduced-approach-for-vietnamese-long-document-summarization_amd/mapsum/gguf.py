@@ -133,6 +133,30 @@ _LAYER = {"attn_q": "wq", "attn_k": "wk", "attn_v": "wv", "attn_output": "wo", "
           "ffn_up": "w_up", "ffn_down": "w_down"}
 
 
+def check_rope_freqs(cfg, ts):
+    """The GGUF's rope_freqs.weight (llama.cpp's llama3 scaling divisors) must be the engine's own
+    table (config.llama3_rope_factors: the cos / sin tables are built from cfg, not from the
+    file), or the model would silently run with another RoPE -- refuse.  A file without the
+    tensor is accepted only for an unscaled config (rope_factor 0)."""
+    from .config import llama3_rope_factors
+    want = llama3_rope_factors(cfg)
+    if "rope_freqs.weight" not in ts:
+        if cfg.rope_factor and cfg.rope_factor > 0:
+            raise GGUFError("no rope_freqs.weight tensor: the engine applies llama3 RoPE scaling "
+                            f"(factor {cfg.rope_factor}); a GGUF without it is another RoPE")
+        return
+    t, d, raw = ts["rope_freqs.weight"]
+    if t in QBLOCK:
+        raise GGUFError("rope_freqs.weight: quantised")
+    got = _rows(t, d, raw).reshape(-1).astype(np.float64)
+    if got.shape != want.shape or not np.allclose(got, want, rtol=1e-5, atol=0.0):
+        bad = int(np.argmax(np.abs(got - want) / want)) if got.shape == want.shape else -1
+        raise GGUFError(f"rope_freqs.weight does not match the engine's llama3 RoPE scaling (theta "
+                        f"{cfg.rope_theta}, factor {cfg.rope_factor}, low/high {cfg.rope_low_freq_factor}/"
+                        f"{cfg.rope_high_freq_factor}, orig ctx {cfg.rope_orig_ctx}): first mismatch at "
+                        f"frequency {bad} -- refusing to run this model with another RoPE")
+
+
 def load_gguf(engine, path: str):
     """Upload a llama-architecture GGUF into ``engine`` (shape checked against engine.cfg)."""
     cfg = engine.cfg
@@ -151,6 +175,7 @@ def load_gguf(engine, path: str):
             raise GGUFError(f"missing tensor {name}")
         return ts[name]
 
+    check_rope_freqs(cfg, ts)
     mats = {"embed": get("token_embd.weight")}
     if "output.weight" in ts and not cfg.tie_embeddings:
         mats["lm_head"] = ts["output.weight"]

@@ -71,8 +71,25 @@ class OllamaModel:
     template: str | None = None
 
 
-def resolve(name: str, root: str | None = None) -> OllamaModel:
-    """Manifest -> blobs of one pulled model (OllamaStoreError if it is not there)."""
+# what a llama3-family chat template must contain for mapsum.template.render_llama32 (the
+# engine's own rendering of Ollama's llama3.2 TEMPLATE) to be the prompt Ollama would build
+LLAMA3_TEMPLATE_MARKERS = ("<|start_header_id|>", "<|end_header_id|>", "<|eot_id|>")
+
+
+def template_problems(text: str) -> list:
+    """Why a manifest's chat template is not the llama3 family the engine renders (empty: it is).
+    The layer is Go template source, so the check is structural: Llama-3's header / end-of-turn
+    markers and a prompt or messages action."""
+    out = [f"no {m!r}" for m in LLAMA3_TEMPLATE_MARKERS if m not in text]
+    if ".Prompt" not in text and ".Messages" not in text:
+        out.append("no .Prompt / .Messages action")
+    return out
+
+
+def resolve(name: str, root: str | None = None, allow_foreign_template: bool = False) -> OllamaModel:
+    """Manifest -> blobs of one pulled model (OllamaStoreError if it is not there, or if its
+    chat template is not the llama3 family mapsum.template renders -- unless
+    allow_foreign_template, or MAPSUM_ALLOW_TEMPLATE=1)."""
     root = root or models_dir()
     host, ns, model, tag = parse_tag(name)
     man = os.path.join(root, "manifests", host, ns, model, tag)
@@ -93,6 +110,12 @@ def resolve(name: str, root: str | None = None) -> OllamaModel:
                 out.template = f.read().decode("utf-8")
     if not out.gguf:
         raise OllamaStoreError(f"manifest {man} has no {MODEL_MEDIA} layer")
+    if out.template is not None:
+        why = template_problems(out.template)
+        if why and not (allow_foreign_template or os.environ.get("MAPSUM_ALLOW_TEMPLATE") == "1"):
+            raise OllamaStoreError(f"model {name!r}: its chat template is not Llama-3's ({'; '.join(why)}); "
+                                   "the engine renders Llama-3.2's template (mapsum/template.py) -- refusing "
+                                   "(MAPSUM_ALLOW_TEMPLATE=1 overrides)")
     if not os.path.isfile(out.gguf):
         raise OllamaStoreError(f"model blob {out.gguf} missing (ollama pull {name})")
     return out

@@ -12,6 +12,9 @@ from __future__ import annotations
 import os
 
 
+_NO_BOS = object()  # from_object(bos_id=_NO_BOS): the vocabulary prepends no BOS at all
+
+
 class Tokenizer:
     def __init__(self, path: str | None = None, bos_id: int | None = None):
         from tokenizers import Tokenizer as _T
@@ -26,7 +29,10 @@ class Tokenizer:
     def from_object(cls, tk, bos_id=None):
         self = cls.__new__(cls)
         self.tk = tk
-        self.bos_id = bos_id if bos_id is not None else tk.token_to_id("<|begin_of_text|>")
+        if bos_id is _NO_BOS:
+            self.bos_id = None
+        else:
+            self.bos_id = bos_id if bos_id is not None else tk.token_to_id("<|begin_of_text|>")
         return self
 
     def encode(self, text: str, add_bos: bool = True) -> list:
@@ -88,9 +94,9 @@ def tokenizer_from_gguf(meta: dict) -> "Tokenizer":
     tk.decoder = decoders.ByteLevel()
     tk.add_special_tokens([AddedToken(tokens[i], special=True, normalized=False)
                            for i, ty in enumerate(types) if ty in (TOKEN_CONTROL, TOKEN_USER_DEFINED)])
-    bos = meta.get("tokenizer.ggml.bos_token_id")
     if not meta.get("tokenizer.ggml.add_bos_token", True):
-        bos = None
+        return Tokenizer.from_object(tk, bos_id=_NO_BOS)  # (None would look <|begin_of_text|> up)
+    bos = meta.get("tokenizer.ggml.bos_token_id")
     return Tokenizer.from_object(tk, bos_id=int(bos) if bos is not None else None)
 
 

@@ -58,11 +58,19 @@ _NAMES = {"wq": "attn_q", "wk": "attn_k", "wv": "attn_v", "wo": "attn_output", "
           "w_up": "ffn_up", "w_down": "ffn_down"}
 
 
+def rope_freqs(cfg=TINY):
+    """llama.cpp's rope_freqs.weight for a llama3-scaled config (the converter's divisors)."""
+    from mapsum.config import llama3_rope_factors
+    f = llama3_rope_factors(cfg).astype(np.float32)
+    return ("rope_freqs.weight", gguf.GGML_F32, [f.size], f.tobytes())
+
+
 def float_gguf(path, w, dtype=np.float32):
     t = gguf.GGML_F32 if dtype == np.float32 else gguf.GGML_F16
     f = lambda a: a.astype(dtype).tobytes()  # noqa: E731
     ts = [("token_embd.weight", t, [TINY.hidden, TINY.vocab], f(w["embed"])),
-          ("output_norm.weight", gguf.GGML_F32, [TINY.hidden], w["final_norm"].astype(np.float32).tobytes())]
+          ("output_norm.weight", gguf.GGML_F32, [TINY.hidden], w["final_norm"].astype(np.float32).tobytes()),
+          rope_freqs()]
     heads = {"wq": TINY.n_heads, "wk": TINY.n_kv_heads}
     for i, ly in enumerate(w["layers"]):
         for n in ("attn_norm", "ffn_norm"):
@@ -103,7 +111,7 @@ def test_float_gguf_loads_logical_weights(tmp_path):
     path = str(tmp_path / "tiny-f32.gguf")
     float_gguf(path, w)
     meta, ts = gguf.read_gguf(path)
-    assert meta["general.name"] == "tiny-test" and len(ts) == 2 + 9 * TINY.n_layers
+    assert meta["general.name"] == "tiny-test" and len(ts) == 3 + 9 * TINY.n_layers
     eng = Recorder()
     gguf.load_gguf(eng, path)
     assert np.array_equal(eng.f16[(L.MS_T_EMBED, 0)], f32_to_f16_bits(w["embed"]))
@@ -123,6 +131,7 @@ def test_quant_gguf_loads_unpermuted_blocks(tmp_path):
     emb = Q.random_blocks(Q.GGML_TYPE_Q6_K, TINY.vocab * TINY.hidden // 256, seed=1).reshape(TINY.vocab, -1)
     ts.append(("token_embd.weight", gguf.GGML_Q6_K, [TINY.hidden, TINY.vocab], emb.tobytes()))
     ts.append(("output_norm.weight", gguf.GGML_F32, [TINY.hidden], np.ones(TINY.hidden, np.float32).tobytes()))
+    ts.append(rope_freqs())
     for i in range(TINY.n_layers):
         for n in ("attn_norm", "ffn_norm"):
             ts.append((f"blk.{i}.{n}.weight", gguf.GGML_F32, [TINY.hidden],
@@ -155,6 +164,29 @@ def test_errors(tmp_path):
     write_gguf(str(p), META, [("token_embd.weight", 2, [32, 4], b"\0" * 72)])  # Q4_0
     with pytest.raises(gguf.GGUFError, match="not supported"):
         gguf.read_gguf(str(p))
+
+
+def test_rope_freqs_must_match_the_engine(tmp_path):
+    """the engine builds its cos / sin tables from its config, so a GGUF whose
+    rope_freqs.weight holds other llama3 divisors (here: another scaling factor), or none at all
+    for a scaled config, is refused instead of silently running with the wrong RoPE."""
+    w = make_weights(TINY, 5, std=0.05, jitter=0.1)
+    good = str(tmp_path / "good.gguf")
+    float_gguf(good, w)
+    gguf.load_gguf(Recorder(), good)
+    meta, ts = gguf.read_gguf(good)
+    other = rope_freqs(TINY.with_(rope_factor=8.0))
+    for name, entries in (("other", [other]), ("missing", [])):
+        p = str(tmp_path / f"{name}.gguf")
+        keep = [(n, t, d, bytes(raw)) for n, (t, d, raw) in ts.items() if n != "rope_freqs.weight"]
+        write_gguf(p, META, keep + entries)
+        with pytest.raises(gguf.GGUFError, match="rope_freqs"):
+            gguf.load_gguf(Recorder(), p)
+    # an unscaled config needs no table
+    class Unscaled(Recorder):
+        cfg = TINY.with_(rope_factor=0.0)
+    p = str(tmp_path / "missing.gguf")
+    gguf.load_gguf(Unscaled(), p)
 
 
 @pytest.mark.gpu

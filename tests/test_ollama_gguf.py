@@ -24,7 +24,7 @@ from mapsum.config import TINY
 from mapsum.engine import RequestQueue, Result
 from mapsum.tokenizer import PRE_TOKENIZERS, Tokenizer, gguf_stop_ids, tokenizer_from_gguf
 from oracle.synth import make_weights
-from test_gguf import META, _NAMES, write_gguf
+from test_gguf import META, _NAMES, rope_freqs, write_gguf
 
 SPECIALS = {4000: "<|begin_of_text|>", 4001: "<|end_of_text|>", 4002: "<|eot_id|>",
             4003: "<|start_header_id|>", 4004: "<|end_header_id|>", 4005: "<|eom_id|>"}
@@ -107,7 +107,7 @@ def tiny_gguf(path, w, tok_meta):
     """TINY weights (F32, Q/K rows permuted as llama.cpp's converter does) + tokenizer metadata."""
     f = lambda a: np.asarray(a, np.float32).tobytes()  # noqa: E731
     ts = [("token_embd.weight", gguf.GGML_F32, [TINY.hidden, TINY.vocab], f(w["embed"])),
-          ("output_norm.weight", gguf.GGML_F32, [TINY.hidden], f(w["final_norm"]))]
+          ("output_norm.weight", gguf.GGML_F32, [TINY.hidden], f(w["final_norm"])), rope_freqs()]
     heads = {"wq": TINY.n_heads, "wk": TINY.n_kv_heads}
     for i, ly in enumerate(w["layers"]):
         for n in ("attn_norm", "ffn_norm"):
@@ -120,13 +120,16 @@ def tiny_gguf(path, w, tok_meta):
     write_gguf(path, meta, ts)
 
 
-def ollama_store_with(root, tag, gguf_path, params):
+def ollama_store_with(root, tag, gguf_path, params, template=None):
     """An Ollama models dir holding one pulled model: manifest + sha256-named blobs."""
     host, ns, model, t = ollama_store.parse_tag(tag)
     os.makedirs(os.path.join(root, "blobs"), exist_ok=True)
     layers = []
-    for media, src in ((ollama_store.MODEL_MEDIA, gguf_path), (ollama_store.PARAMS_MEDIA, None)):
-        data = open(src, "rb").read() if src else json.dumps(params).encode()
+    items = [(ollama_store.MODEL_MEDIA, open(gguf_path, "rb").read()),
+             (ollama_store.PARAMS_MEDIA, json.dumps(params).encode())]
+    if template is not None:
+        items.append((ollama_store.TEMPLATE_MEDIA, template.encode()))
+    for media, data in items:
         dg = hashlib.sha256(data).hexdigest()
         open(os.path.join(root, "blobs", f"sha256-{dg}"), "wb").write(data)
         layers.append({"mediaType": media, "digest": f"sha256:{dg}", "size": len(data)})
@@ -149,6 +152,42 @@ def store(trained, tmp_path_factory):
     ollama_store_with(str(root), "llama3.2:3b", g, PARAMS)
     os.remove(g)  # only the content-addressed blob remains, as in a real store
     return str(root), w
+
+
+# Ollama's llama3.2 chat template source is EXT (not offline): a llama3-family stand-in with the
+# same structure (Go template actions, Llama-3 header / end-of-turn markers), and a ChatML one
+LLAMA3_LIKE = ("{{- range .Messages }}<|start_header_id|>{{ .Role }}<|end_header_id|>\n\n{{ .Content }}"
+               "<|eot_id|>{{ end }}<|start_header_id|>assistant<|end_header_id|>\n\n")
+CHATML = "{{- range .Messages }}<|im_start|>{{ .Role }}\n{{ .Content }}<|im_end|>\n{{ end }}<|im_start|>assistant\n"
+
+
+def test_resolve_checks_the_template(tmp_path, store):
+    """the manifest's template layer is read and checked -- a llama3-family
+    template resolves, any other family is refused (the engine renders Llama-3.2's template
+    itself, mapsum/template.py), unless explicitly allowed."""
+    root, _ = store
+    blob = ollama_store.resolve("llama3.2:3b", root).gguf
+    for tag, tmpl in (("llama3.2:ok", LLAMA3_LIKE), ("llama3.2:chatml", CHATML)):
+        ollama_store_with(root, tag, blob, PARAMS, template=tmpl)
+    assert ollama_store.template_problems(LLAMA3_LIKE) == []
+    m = ollama_store.resolve("llama3.2:ok", root)
+    assert m.template == LLAMA3_LIKE
+    with pytest.raises(ollama_store.OllamaStoreError, match="template is not Llama-3"):
+        ollama_store.resolve("llama3.2:chatml", root)
+    assert ollama_store.resolve("llama3.2:chatml", root, allow_foreign_template=True).template == CHATML
+
+
+def test_gguf_add_bos_token_false(trained):
+    """tokenizer.ggml.add_bos_token = false really disables BOS (it used to fall back
+    to looking <|begin_of_text|> up)."""
+    _, tok_meta = trained
+    with_bos = tokenizer_from_gguf(tok_meta)
+    no_bos = tokenizer_from_gguf(dict(tok_meta, **{"tokenizer.ggml.add_bos_token": False}))
+    text = "xin chao the gioi"
+    assert no_bos.bos_id is None
+    assert no_bos.encode(text) == with_bos.encode(text, add_bos=False)
+    if with_bos.bos_id is not None:
+        assert with_bos.encode(text)[0] == with_bos.bos_id
 
 
 def test_resolve_and_config(store):
