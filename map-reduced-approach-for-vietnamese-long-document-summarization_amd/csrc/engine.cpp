@@ -30,7 +30,12 @@
 #include <string>
 #include <vector>
 
+#if MS_HAVE_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
+#else  // no rocprofiler-sdk-roctx: the trace ranges compile to nothing
+static inline int roctxRangePushA(const char*) { return 0; }
+static inline int roctxRangePop() { return 0; }
+#endif
 
 #include "kernels.h"
 #include "mapsum.h"
@@ -193,6 +198,11 @@ struct ms_engine {
   unsigned* pk_err_h = nullptr;  // pinned copy
   f16_t* pk_xg2 = nullptr;       // [max_batch][H] gate/up input
   float* pk_ssq2 = nullptr;      // [256][max_batch] its statistics
+  // the layers' matrices in the step's stream order (launch_pack_layer; 201 MB per layer),
+  // allocated at the first persistent run and rebuilt after any weight (re)load -- including a
+  // broadcast into the regions ms_weight_regions hands out
+  char* pk_packed = nullptr;
+  mutable bool pk_packed_ok = false;
   bool persist_on(int B) const {
     return persist && persist_ok && !overlap && B >= 1 && B <= cfg.max_batch && !has_quant &&
            attn2_ok(B, max_pages * kPage) && attn_slabs && resid_fused(nullptr) && split_qkv == 6;
@@ -662,6 +672,7 @@ struct ms_engine {
   // Captured decode graphs bake in the weight form (fp16 vs K-quant stream) and the split
   // choices: any weight (re)load invalidates them.
   void drop_graphs() {
+    pk_packed_ok = false;
     for (auto& kv : decode_graphs) (void)hipGraphExecDestroy(kv.second.first);
     decode_graphs.clear();
   }
@@ -1122,6 +1133,7 @@ int ms_quant_manifest(const ms_engine* e, int32_t* triples, int32_t cap) {
 
 int ms_weight_regions(const ms_engine* e, void** ptrs, int64_t* bytes, int32_t cap) {
   if (!e || cap < 0 || (cap > 0 && (!ptrs || !bytes))) return MS_EINVAL;
+  e->pk_packed_ok = false;  // the caller may write into the regions (weight broadcast)
   const auto r = e->weight_regions();
   for (int i = 0; i < std::min((int)r.size(), (int)cap); ++i) {
     ptrs[i] = r[i].first;
@@ -1451,7 +1463,8 @@ static void persist_layers(ms_engine& E, int B, const DecodeAttnArgs& da) {
     const Layer& Ly = E.layers[l];
     const KVView kv = E.kv_layer(l);
     a.layers[l] = PkLayer{Ly.wqkv, Ly.wo, Ly.wgu, Ly.wdown, Ly.ffn_norm,
-                          l + 1 < E.L ? E.layers[l + 1].attn_norm : E.final_norm, kv.k, kv.v};
+                          l + 1 < E.L ? E.layers[l + 1].attn_norm : E.final_norm, kv.k, kv.v,
+                          E.pk_packed + (size_t)l * persist_packed_bytes_per_layer()};
   }
   a.L = E.L;
   a.B = B;
@@ -1550,6 +1563,30 @@ static void decode_run(ms_engine& E, std::vector<Seq*>& batch, int k, std::vecto
   // the persistent step runs (captured or eagerly) exactly when persist_on holds for this run;
   // toggling it drops the cached graphs (ms_set_persist, the timeout fallback below)
   E.pk_used = E.persist_on(B);
+  if (E.pk_used && !E.pk_packed_ok) {
+    // its weights in stream order: allocated once (the engine falls back to the launches if
+    // the 5.6 GB do not fit), rebuilt from the [N][K] matrices after every weight (re)load
+    if (!E.pk_packed) {
+      void* p = nullptr;
+      if (hipMalloc(&p, persist_packed_bytes_per_layer() * E.L) == hipSuccess) {
+        E.pk_packed = (char*)p;
+        E.allocs.push_back(p);
+      } else {
+        (void)hipGetLastError();
+        E.persist = false;
+        E.pk_used = false;
+      }
+    }
+    if (E.pk_used) {
+      for (int l = 0; l < E.L; ++l) {
+        const Layer& Ly = E.layers[l];
+        launch_pack_layer(Ly.wqkv, Ly.wo, Ly.wgu, Ly.wdown, E.pk_packed + (size_t)l * persist_packed_bytes_per_layer(),
+                          E.stream);
+      }
+      HIP_OK(hipGetLastError());
+      E.pk_packed_ok = true;
+    }
+  }
   HIP_OK(hipEventRecord(E.ev_a, E.stream));
   int32_t* d = E.upload_args(a);
   decode_head(E, B, d);  // the first step's input; each step's tail gathers the next one's

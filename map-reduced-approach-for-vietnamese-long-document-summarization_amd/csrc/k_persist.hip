@@ -43,15 +43,30 @@ namespace pk {
 constexpr int H = 3072, F = 8192, HQ = 24, HK = 8, G = 3, D = 128;
 constexpr int QKVN = (HQ + 2 * HK) * D;  // 5120
 constexpr int NCU = 256;
-constexpr int NTHR = 256;  // wave 0 loader, waves 1-3 consumers
-constexpr int NCW = 3;
+constexpr int NTHR = 256;  // waves 0-1 loaders, waves 2-3 consumers
+constexpr int NLD = 2;     // loader waves: one wave issuing LDS DMA tops out at ~14 GB/s per CU, two
+                           // reach ~23 (tools/dma_probe.hip, profiles/r06/dma_probe.txt)
+constexpr int NCW = 2;
+// DMA instructions (KiB) each loader keeps in flight: two loaders at 8 each already stream ~23 GB/s
+// per CU (dma_probe), and a deeper queue only delays every other memory operation of the CU (a
+// consumer's publish drain, a poll, a gather) behind it -- the CU serves them in order
+constexpr int DEPTH = 12;
 constexpr int MAXB = 8;
 constexpr int R = 6;  // ring slots
 constexpr int SLOT = 16384;
 constexpr int RT = 12;                // O / down rows per tile (H / NCU)
 constexpr int QS = 6;                 // QKV split-K slabs of 512 k
-constexpr int QUG = 40 * QS;          // 240 units per kv group
+constexpr int QUG = 40 * QS;          // 240 units per kv group (on the 32 CUs of XCD g)
 constexpr int PPB_MAX = 9;
+// The weights in STREAM order (pack_layer_kernel): every ring slot of a layer is one contiguous
+// block whose bytes are already in the slot's LDS order (chunk swizzle applied), so a fill is a
+// straight 1-KiB-per-instruction copy -- read in [N][K] order a gate/up slot was 32 pieces of
+// 384 B, 6 KiB apart, and streamed at half the rate of a contiguous K / V page
+constexpr size_t PK_QKV = (size_t)8 * QUG * 16384;  // [kv group][unit][16 rows x 512 k]
+constexpr size_t PK_O = (size_t)NCU * 8 * 9216;      // [cu][slot][12 rows x 384 k]
+constexpr size_t PK_GU = (size_t)NCU * 32 * 12288;   // [cu][slot][32 rows x 192 k]
+constexpr size_t PK_DN = (size_t)NCU * 16 * 12288;   // [cu][slot][12 rows x 512 k]
+constexpr size_t PK_LAYER = PK_QKV + PK_O + PK_GU + PK_DN;
 
 // LDS map (bytes)
 constexpr int L_RING = 0;
@@ -65,9 +80,9 @@ constexpr int MAXL = 28;
 constexpr int L_RINV = L_GAM + MAXL * 2 * RT * 2;
 constexpr int L_SEQ = L_RINV + 32;          // len[8], slot[8], nsplit[8]
 constexpr int L_CTL = L_SEQ + 96;
-constexpr int L_PQ = L_CTL + 256;           // the loader's queue of issued fills: end, flag, value
+constexpr int L_PQ = L_CTL + 256;           // each loader's queue of issued fills: end, flag, value
 constexpr int PQN = 16;
-constexpr int L_END = L_PQ + PQN * 12;
+constexpr int L_END = L_PQ + NLD * PQN * 12;
 static_assert(L_END <= 160 * 1024, "LDS");
 // attention scratch inside the X region
 constexpr int A_SL = 0;                     // gathered QKV slab values [6][(G+2)*128] f32
@@ -79,10 +94,13 @@ constexpr int A_MW = A_QN + (G + 2) * D * 2;   // per page: [G][130] f32 (m, l, 
 constexpr int MWP = G * 130 * 4;
 static_assert(A_MW + PPB_MAX * MWP <= XBYTES, "attention scratch");
 // control words (ints at L_CTL)
+// C_XCNT / C_HCNT count completed HALVES of the split fills (each loader wave adds one per fill);
+// C_RDY: the latest chip-wide edge loader 0 saw (4 l + j), which loader 1 waits on instead of polling
 enum {
-  C_FULL = 0, C_FREE = R, C_XSEQ = 2 * R, C_PROSEQ, C_PRODONE, C_ITEMDONE, C_QKVDONE, C_PAGESDONE,
-  C_HFULL, C_HFREE = C_HFULL + 3, C_TICK = C_HFREE + 3, C_RINV, C_ABORT, C_LAST, C_NCTL
+  C_FULL = 0, C_FREE = R, C_XCNT = 2 * R, C_PROSEQ, C_PRODONE, C_ITEMDONE, C_QKVDONE, C_PAGESDONE,
+  C_HCNT, C_HFREE = C_HCNT + 3, C_TICK = C_HFREE + 3, C_RINV, C_ABORT, C_LAST, C_RDY, C_NCTL
 };
+constexpr int kAddOne = -0x7fffffff;  // pending-queue value: atomically add 1 to the flag word
 static_assert(C_NCTL * 4 <= 256, "control words");
 // global sync words per layer
 constexpr int SL = 128;
@@ -117,6 +135,17 @@ __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ void dma16(const void* src, const char* lds) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS_AS const char*)lds);
   asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"{m0}"(m0), "v"(src) : "memory");
+}
+// the loader's throttle after each DMA instruction: at most `depth` in flight (wave-uniform; a
+// scalar branch per instruction)
+__device__ __forceinline__ void throttle(int depth) {
+  if (depth <= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (depth <= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (depth <= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (depth <= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+  else if (depth <= 28) asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+  else if (depth <= 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(44)" ::: "memory");
 }
 // coherent (sc1) DMA of bytes other workgroups wrote in this launch (behind their counters)
 __device__ __forceinline__ void dma16c(const void* src, const char* lds) {
@@ -200,13 +229,15 @@ struct Loader {
   unsigned* err;
   unsigned spin;
   int lane;
+  int ldr;     // loader index: issues the ring slots k with k % NLD == ldr and instruction i % NLD == ldr of fills
+  int depth;   // DMA instructions kept in flight by the throttle
   int issued;  // DMA instructions issued
   int head, tail;
   int k;         // next ring slot
   int done_end;  // every DMA instruction before this one has landed
   unsigned long long* st;  // diagnostic trace (stamps on)
   int cu, tbase;           // trace: this CU, the traced layer's first slot
-  __device__ __forceinline__ int* pq() { return (int*)(smem + L_PQ); }
+  __device__ __forceinline__ int* pq() { return (int*)(smem + L_PQ + ldr * PQN * 12); }
   // keep the wave's outstanding DMA instructions <= 62 (vmcnt is 6 bits) before issuing n more
   __device__ __forceinline__ void make_room(int n) {
     while (head != tail && issued - done_end + n > 62) retire_one();
@@ -233,7 +264,10 @@ struct Loader {
     const int val = __builtin_amdgcn_readfirstlane(q[3 * e + 2]);
     wait_vm(issued - end);
     cbar();
-    if (lane == 0) PK_CTL(fi) = val;
+    if (lane == 0) {
+      if (val == kAddOne) atomicAdd((int*)(smem + L_CTL + 4 * fi), 1);
+      else PK_CTL(fi) = val;
+    }
     head += 1;
     done_end = end;
     if (fi < R) pk_trace(st, cu, val - tbase, kTraceLayer, 1);
@@ -241,9 +275,9 @@ struct Loader {
   __device__ __forceinline__ void retire_all() {
     while (head != tail) retire_one();
   }
-  // keep ~40 KiB in flight: groups that far behind the issue head are published
+  // groups at least DEPTH instructions behind the issue head have landed (throttle): publish them
   __device__ __forceinline__ void retire_lag() {
-    while (head != tail && issued - __builtin_amdgcn_readfirstlane(pq()[3 * (head & (PQN - 1))]) >= 40) retire_one();
+    while (head != tail && issued - __builtin_amdgcn_readfirstlane(pq()[3 * (head & (PQN - 1))]) >= depth) retire_one();
     while (tail - head >= PQN - 2) retire_one();
   }
   // wait until LDS word idx >= v, publishing landed fills meanwhile
@@ -283,6 +317,20 @@ struct Loader {
       __builtin_amdgcn_s_sleep(4);
     }
   }
+  // chip-wide edge e (4 l + j): loader 0 polls the n counters at p and publishes e in LDS; loader 1
+  // waits for that word (one poller per CU: polling-cost)
+  __device__ __forceinline__ bool wait_edge(int e, const unsigned* p, int n, unsigned target, unsigned code) {
+    if (ldr == 0) {
+      if (p && !wait_glb(p, n, target, code)) return false;
+      cbar();
+      if (lane == 0) PK_CTL(C_RDY) = e;
+      return true;
+    }
+    return wait_lds(C_RDY, e, code + 0x10);
+  }
+  // ring slots are owned by parity: the other loader's slots are only counted
+  __device__ __forceinline__ bool mine() const { return k % NLD == ldr; }
+  __device__ __forceinline__ void skip() { k += 1; }
   // the next ring slot's position is free once slot k - R was released
   __device__ __forceinline__ char* ring_slot() {
     const int pos = k % R;
@@ -296,25 +344,23 @@ struct Loader {
     k += 1;
     retire_lag();
   }
-  // weight tile: NROWS rows from row0, S 16-B chunks per row (k0.. k0 + 8S), into one slot with
-  // the chunk swizzle the consumers read (S % 16 == 0: chunk ^ (r & 15); else chunk ^ ((r >> 1) & 7))
-  template <int NROWS, int S>
-  __device__ __forceinline__ void w_slot(const f16_t* W, int K, int row0, int k0) {
+  // a packed weight slot (NI KiB, contiguous, already in LDS order) into the next ring position
+  template <int NI>
+  __device__ __forceinline__ void w_slot(const char* src) {
+    if (!mine()) return skip();
     char* dst = ring_slot();
     if (aborted(smem)) return;
-    constexpr int NI = NROWS * S / 64;
-    static_assert(NROWS * S % 64 == 0, "whole DMA instructions");
     make_room(NI);
 #pragma unroll 4
     for (int i = 0; i < NI; ++i) {
-      const int P = i * 64 + lane, r = P / S, ch = P - r * S;
-      const int C = ch ^ ((S % 16 == 0) ? (r & 15) : ((r >> 1) & 7));
-      dma16(W + (size_t)(row0 + r) * K + k0 + C * 8, dst + i * 1024);
+      dma16(src + i * 1024 + lane * 16, dst + i * 1024);
+      throttle(depth);
     }
     ring_done(NI);
   }
   // K page (k_swz layout) or V page (v_swz layout, k_attn.hip attn_decode2's DMA mapping)
   __device__ __forceinline__ void kv_slot(const f16_t* base, bool is_v) {
+    if (!mine()) return skip();
     char* dst = ring_slot();
     if (aborted(smem)) return;
     make_room(16);
@@ -323,20 +369,25 @@ struct Loader {
       const int rr = 4 * i + (lane >> 4);
       const int ch = is_v ? ((lane & 15) ^ ((rr & 7) << 1)) : ((lane & 15) ^ (rr & 15));
       dma16(base + rr * D + ch * 8, dst + i * 1024);
+      throttle(depth);
     }
     ring_done(16);
   }
-  // X image of rows [0, B) x k [k0, k0 + K) of a [B][ld] fp16 matrix (gemv_common.h x_lds layout)
+  // this loader's half of the X image of rows [0, B) x k [k0, k0 + K) of a [B][ld] fp16 matrix
+  // (gemv_common.h x_lds layout): instructions i % NLD == ldr.  Not throttled: a hand-off gather
+  // sits on the edge's critical path and its coherent (sc1) reads take ~3 us each, so all of them
+  // go out at once (one round trip; the weight slots keep DEPTH)
   __device__ __forceinline__ int x_fill(const f16_t* X, int B, int K, int ld, int k0, char* dst) {
     const int kch = K >> 3, n = B * kch, ni = (n + 63) / 64;
-    make_room(ni);
-    for (int i = 0; i < ni; ++i) {
+    const int mine_n = (ni - ldr + NLD - 1) / NLD;
+    make_room(mine_n);
+    for (int i = ldr; i < ni; i += NLD) {
       const int P = min(i * 64 + lane, n - 1);
       const int r = P / kch, c = P - r * kch;
       dma16c(X + (size_t)r * ld + k0 + ((c ^ (r & 7)) << 3), dst + i * 1024);
     }
-    issued += ni;
-    return ni;
+    issued += mine_n;
+    return mine_n;
   }
 };
 
@@ -441,7 +492,9 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
     for (int p = 0; p < R; ++p) PK_CTL(C_FREE + p) = -1;
     PK_CTL(C_QKVDONE) = 0;
     PK_CTL(C_PAGESDONE) = 0;
+    PK_CTL(C_XCNT) = 0;
     for (int p = 0; p < 3; ++p) PK_CTL(C_HFREE + p) = 0;
+    for (int p = 0; p < 3; ++p) PK_CTL(C_HCNT + p) = 0;
     PK_CTL(C_TICK) = 0;
     PK_CTL(C_ABORT) = 0;
   }
@@ -463,28 +516,32 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
   const int NSL = nq + natt + 8 + 32 + 16;  // ring slots per layer
   const int tiles0 = a.rs0_tiles;
 
-  if (wave == 0) {
-    // ================================================================ loader
-    Loader ld{smem, a.err, a.spin, lane, 0, 0, 0, 0, 0, a.stamps, c, kTraceLayer * NSL};
+  if (wave < NLD) {
+    // ================================================================ loaders
+    Loader ld{smem, a.err, a.spin, lane, wave, a.depth, 0, 0, 0, 0, 0, a.stamps, c, kTraceLayer * NSL};
     for (int l = 0; l < a.L && !aborted(smem); ++l) {
       const PkLayer Ly = a.layers[l];
       unsigned* sy = a.sync + (size_t)l * SL;
-      PK_STAMP(l, 0);
+      if (wave == 0) PK_STAMP(l, 0);
       // -- QKV: unit slots; the X image (xb) once the previous layer's down tiles are all in
       auto x_qkv = [&]() __attribute__((always_inline)) {
-        if (l > 0 && !ld.wait_glb(a.sync + (size_t)(l - 1) * SL + S_DN, 8, 32, 0x301)) return;
-        PK_STAMP(l, 1);
+        if (!ld.wait_edge(4 * l, l > 0 ? a.sync + (size_t)(l - 1) * SL + S_DN : nullptr, 8, 32, 0x301)) return;
+        if (wave == 0) PK_STAMP(l, 1);
         ld.x_fill(a.xb, B, H, H, 0, smem + L_X);
-        ld.push(C_XSEQ, 3 * l);
+        ld.push(C_XCNT, kAddOne);
+        ld.retire_lag();
       };
       for (int i = 0; i < nq; ++i) {
         if (i == min(R, nq)) x_qkv();
         int tile, slab, grp;
         qkv_unit(c, i, tile, slab, grp);
-        ld.w_slot<16, 64>(Ly.wqkv, H, 16 * tile, slab * 512);
+        ld.w_slot<16>(Ly.packed + ((size_t)(c & 7) * QUG + (c >> 3) + 32 * i) * 16384);
+        (void)tile;
+        (void)slab;
+        (void)grp;
       }
       if (nq <= R) x_qkv();
-      // -- attention items: K / V page slots; the item's QKV slab values once its group is in
+      // -- attention items: K / V page slots; the item's QKV slab values (loader 0) once its group is in
       int it_ord = l * nit;
       for (int idx = c; idx < n_items; idx += NCU) {
         int b, g, s;
@@ -492,11 +549,12 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
         const int npg = item_pages(smem, a.ppb, b, s);
         const int slot = sq[8 + b], len = sq[b], pos = len - 1;
         auto gather = [&]() __attribute__((always_inline)) {
+          if (wave != 0) return;
           // this CU's QKV units are done with the X image, and the previous item's prologue with
           // the slab area; then the group's 240 QKV units
           if (!ld.wait_lds(C_QKVDONE, nq * (l + 1), 0x102)) return;
           if (!ld.wait_lds(C_PRODONE, it_ord - 1, 0x103)) return;
-          if (!ld.wait_glb(sy + S_QKV + g, 1, QUG, 0x302)) return;
+          if (!ld.wait_glb(sy + S_QKV + g, 1, 32 * NCW, 0x302)) return;
           PK_STAMP(l, 2);
           char* ax = smem + L_X;
           const int tiles = l == 0 ? tiles0 : NCU;
@@ -531,54 +589,55 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       // -- O: tile c, 8 slots of 2 chunks; the attention output once every (b, g) is in
       for (int j = 0; j < 8; ++j) {
         if (j == min(R, 8)) {
-          if (ld.wait_glb(sy + S_ATT, 1, (unsigned)(B * HK), 0x303)) {
-            PK_STAMP(l, 3);
+          if (ld.wait_edge(4 * l + 1, sy + S_ATT, 1, (unsigned)(B * HK), 0x303)) {
+            if (wave == 0) PK_STAMP(l, 3);
             ld.x_fill(a.attn, B, H, H, 0, smem + L_X);
-            ld.push(C_XSEQ, 3 * l + 1);
+            ld.push(C_XCNT, kAddOne);
+            ld.retire_lag();
           }
         }
-        ld.w_slot<RT, 48>(Ly.wo, H, RT * c, 384 * j);
+        ld.w_slot<9>(Ly.packed + PK_QKV + ((size_t)c * 8 + j) * 9216);
       }
       // -- gate/up: tiles c, c + 256, 16 chunks each; xg2 + statistics once every O tile is in
       for (int j = 0; j < 32; ++j) {
         if (j == R) {
-          if (ld.wait_glb(sy + S_O, 8, 32, 0x304)) {
-            PK_STAMP(l, 4);
+          if (ld.wait_edge(4 * l + 2, sy + S_O, 8, 32, 0x304)) {
+            if (wave == 0) PK_STAMP(l, 4);
             ld.x_fill(a.xg2, B, H, H, 0, smem + L_X);
-            ld.make_room(B);
-            for (int i = 0; i < B; ++i) dma16c(a.ssq2 + i * 256 + lane * 4, smem + L_SSQ + i * 1024);
-            ld.issued += B;
-            ld.push(C_XSEQ, 3 * l + 2);
+            const int mine_b = (B - wave + NLD - 1) / NLD;
+            ld.make_room(mine_b);
+            for (int i = wave; i < B; i += NLD) dma16c(a.ssq2 + i * 256 + lane * 4, smem + L_SSQ + i * 1024);
+            ld.issued += mine_b;
+            ld.push(C_XCNT, kAddOne);
           }
         }
-        const int tg = c + NCU * (j >> 4);
-        ld.w_slot<32, 24>(Ly.wgu, H, 32 * tg, 192 * (j & 15));
+        ld.w_slot<12>(Ly.packed + PK_QKV + PK_O + ((size_t)c * 32 + j) * 12288);
       }
       // -- down: tile c, 16 chunks of 512 k; h through the 3-slot ring in the X region
       auto h_slot = [&](int i) __attribute__((always_inline)) {  // h columns [1024 i, +1024)
         const int hi = l * 8 + i, pos = hi % 3;
         if (!ld.wait_lds(C_HFREE + pos, 2 * (hi / 3), 0x104)) return;
         ld.x_fill(a.hbuf, B, 1024, F, 1024 * i, smem + L_X + pos * 16384);
-        ld.push(C_HFULL + pos, hi);
+        ld.push(C_HCNT + pos, kAddOne);
       };
       for (int j = 0; j < 16; ++j) {
         if (j == R) {
-          if (ld.wait_glb(sy + S_GU, 8, 64, 0x305)) {
-            PK_STAMP(l, 5);
+          if (ld.wait_edge(4 * l + 3, sy + S_GU, 8, 64, 0x305)) {
+            if (wave == 0) PK_STAMP(l, 5);
             h_slot(0);
             h_slot(1);
             h_slot(2);
           }
         }
         if (j >= R && !(j & 1) && j / 2 >= 3) h_slot(j / 2);
-        ld.w_slot<RT, 64>(Ly.wdown, F, RT * c, 512 * j);
+        ld.w_slot<12>(Ly.packed + PK_QKV + PK_O + PK_GU + ((size_t)c * 16 + j) * 12288);
       }
-      PK_STAMP(l, 6);
+      if (wave == 0) PK_STAMP(l, 6);
     }
     ld.retire_all();
   } else {
     // ================================================================ consumers
-    const int cw = wave - 1;
+    const int cw = wave - NLD;
     int tick0 = 0;   // ordered chunks before this tile
     int pages_cum = 0;
     for (int l = 0; l < a.L && !aborted(smem); ++l) {
@@ -590,7 +649,7 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       int ndone = 0;
       for (int i = cw; i < nq; i += NCW) {
         const int k = base + i;
-        if (!lds_wait(smem, C_XSEQ, 3 * l, a.err, 0x401)) break;
+        if (!lds_wait(smem, C_XCNT, NLD * (3 * l + 1), a.err, 0x401)) break;
         if (!lds_wait(smem, C_FULL + k % R, k, a.err, 0x402)) break;
         PK_TR(k, 2);
         int tile, slab, grp;
@@ -615,9 +674,12 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
           const int b = 4 * fg + jj;
           if (b < B) st_f32_sc1(a.slabs + ((size_t)slab * B + b) * QKVN + 16 * tile + fr, tot[jj]);
         }
-        arrive(sy + S_QKV + grp);
         ndone += 1;
       }
+      // one arrival per consumer wave after all its units (every unit of CU c is kv group c % 8):
+      // the group is complete only with its last unit anyway, and each drain waits behind the
+      // CU's in-flight DMA
+      if (ndone) arrive(sy + S_QKV + (c & 7));
       if (lane == 0 && ndone) atomicAdd((int*)(smem + L_CTL + 4 * C_QKVDONE), ndone);
       PK_STAMP(l, 7 + (cw == 0 ? 0 : 8));
       // ---------------- attention items
@@ -810,17 +872,28 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
             old = __builtin_amdgcn_readfirstlane(old);
             last = old == (unsigned)(nsb - 1);
             if (last) {
+              // (attn_decode_combine_kernel's arithmetic; every partial this lane needs is loaded
+              // before the first is used: the loads queue behind the CU's DMA, one round trip)
+              constexpr int QM = 8;
               for (int id = lane; id < G * D; id += 64) {
                 const int cc = id >> 7, d = id & 127;
                 const float* p = a.ws + ((size_t)b * HQ + g * G + cc) * a.nsplit_ws * 132;
+                float mq[QM], lq[QM], oq[QM];
+#pragma unroll
+                for (int q = 0; q < QM; ++q) {
+                  const int qq = min(q, nsb - 1);
+                  mq[q] = ld_f32_sc1(p + qq * 132);
+                  lq[q] = ld_f32_sc1(p + qq * 132 + 1);
+                  oq[q] = ld_f32_sc1(p + qq * 132 + 2 + d);
+                }
                 float M = -INFINITY;
-                for (int q = 0; q < nsb; ++q) M = fmaxf(M, ld_f32_sc1(p + q * 132));
+                for (int q = 0; q < nsb; ++q) M = fmaxf(M, q < QM ? mq[q] : ld_f32_sc1(p + q * 132));
                 float Lq = 0.f, O = 0.f;
                 for (int q = 0; q < nsb; ++q) {
-                  const float m_q = ld_f32_sc1(p + q * 132);
+                  const float m_q = q < QM ? mq[q] : ld_f32_sc1(p + q * 132);
                   const float f = m_q == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_q - M);
-                  Lq += f * ld_f32_sc1(p + q * 132 + 1);
-                  O += f * ld_f32_sc1(p + q * 132 + 2 + d);
+                  Lq += f * (q < QM ? lq[q] : ld_f32_sc1(p + q * 132 + 1));
+                  O += f * (q < QM ? oq[q] : ld_f32_sc1(p + q * 132 + 2 + d));
                 }
                 st_f16_sc1(a.attn + (size_t)b * HQ * D + (g * G + cc) * D + d, f2h(O / Lq));
               }
@@ -838,7 +911,7 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       const f16_t* gam = (const f16_t*)(smem + L_GAM) + l * 2 * RT;
       for (int j = cw; j < 8; j += NCW) {
         const int kk = base + nq + natt + j;
-        if (!lds_wait(smem, C_XSEQ, 3 * l + 1, a.err, 0x411)) break;
+        if (!lds_wait(smem, C_XCNT, NLD * (3 * l + 2), a.err, 0x411)) break;
         if (!lds_wait(smem, C_FULL + kk % R, kk, a.err, 0x412)) break;
         PK_TR(kk, 2);
         const char* sl = smem + L_RING + (kk % R) * SLOT;
@@ -875,7 +948,7 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       }
       tick0 += 16;
       // ---------------- gate/up tiles c, c + 256: 32 slots of one chunk (3 steps)
-      if (cw == 0 && lds_wait(smem, C_XSEQ, 3 * l + 2, a.err, 0x421)) {
+      if (cw == 0 && lds_wait(smem, C_XCNT, NLD * (3 * l + 3), a.err, 0x421)) {
         // the rows' deferred-norm factors from the 256 statistics tiles (gemv_common.h rs_finish)
         const float* st = (const float*)(smem + L_SSQ);
         const RowScale rs{nullptr, NCU, H, a.eps, a.inv_h};
@@ -891,7 +964,7 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       }
       for (int j = cw; j < 32; j += NCW) {
         const int kk = base + nq + natt + 8 + j;
-        if (!lds_wait(smem, C_XSEQ, 3 * l + 2, a.err, 0x422)) break;
+        if (!lds_wait(smem, C_XCNT, NLD * (3 * l + 3), a.err, 0x422)) break;
         if (!lds_wait(smem, C_FULL + kk % R, kk, a.err, 0x423)) break;
         PK_TR(kk, 2);
         const char* sl = smem + L_RING + (kk % R) * SLOT;
@@ -939,7 +1012,7 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
       for (int j = cw; j < 16; j += NCW) {
         const int kk = base + nq + natt + 40 + j;
         const int hi = l * 8 + j / 2, hp = hi % 3;
-        if (!lds_wait(smem, C_HFULL + hp, hi, a.err, 0x431)) break;
+        if (!lds_wait(smem, C_HCNT + hp, NLD * (hi / 3 + 1), a.err, 0x431)) break;
         if (!lds_wait(smem, C_FULL + kk % R, kk, a.err, 0x432)) break;
         PK_TR(kk, 2);
         const char* sl = smem + L_RING + (kk % R) * SLOT;
@@ -988,6 +1061,50 @@ __global__ __launch_bounds__(NTHR, 1) void decode_step_kernel(PkArgs a) {
     for (int i = tid; i <= a.L * SL; i += NTHR) __hip_atomic_store((gu32_t*)(a.sync + i), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---------------------------------------------------------------- stream layout
+// one 16-B chunk of the packed layer per thread: slot bytes in the LDS order Loader::w_slot's
+// consumers read (ldw<S>: chunk C of row r at position C ^ (S % 16 ? (r >> 1) & 7 : r & 15))
+__global__ __launch_bounds__(256) void pack_layer_kernel(const f16_t* __restrict__ wqkv, const f16_t* __restrict__ wo,
+                                                         const f16_t* __restrict__ wgu, const f16_t* __restrict__ wdown,
+                                                         char* __restrict__ out) {
+  const size_t X = (size_t)blockIdx.x * 256 + threadIdx.x;  // output chunk
+  if (X >= PK_LAYER / 16) return;
+  size_t x = X * 16;
+  const f16_t* src;
+  if (x < PK_QKV) {
+    const int slot = (int)(x / 16384), P = (int)(x % 16384) / 16;
+    const int g = slot / QUG, u = slot % QUG, tl = u / QS, slab = u % QS;
+    const int tile = tl < 24 ? 24 * g + tl : (tl < 32 ? 192 + 8 * g + (tl - 24) : 256 + 8 * g + (tl - 32));
+    const int r = P / 64, ch = P % 64, C = ch ^ (r & 15);
+    src = wqkv + (size_t)(16 * tile + r) * H + slab * 512 + C * 8;
+  } else if ((x -= PK_QKV) < PK_O) {
+    const int slot = (int)(x / 9216), P = (int)(x % 9216) / 16;
+    const int cu = slot / 8, j = slot % 8;
+    const int r = P / 48, ch = P % 48, C = ch ^ (r & 15);
+    src = wo + (size_t)(RT * cu + r) * H + 384 * j + C * 8;
+  } else if ((x -= PK_O) < PK_GU) {
+    const int slot = (int)(x / 12288), P = (int)(x % 12288) / 16;
+    const int cu = slot / 32, j = slot % 32, tg = cu + NCU * (j >> 4);
+    const int r = P / 24, ch = P % 24, C = ch ^ ((r >> 1) & 7);
+    src = wgu + (size_t)(32 * tg + r) * H + 192 * (j & 15) + C * 8;
+  } else {
+    x -= PK_GU;
+    const int slot = (int)(x / 12288), P = (int)(x % 12288) / 16;
+    const int cu = slot / 16, j = slot % 16;
+    const int r = P / 64, ch = P % 64, C = ch ^ (r & 15);
+    src = wdown + (size_t)(RT * cu + r) * F + 512 * j + C * 8;
+  }
+  *(uint4*)(out + X * 16) = *(const uint4*)src;
+}
+
+size_t persist_packed_bytes_per_layer() { return PK_LAYER; }
+
+void launch_pack_layer(const f16_t* wqkv, const f16_t* wo, const f16_t* wgu, const f16_t* wdown, void* out,
+                       hipStream_t s) {
+  const size_t n = PK_LAYER / 16;
+  MS_LAUNCH(pack_layer_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, wqkv, wo, wgu, wdown, (char*)out);
+}
+
 // ---------------------------------------------------------------- host
 size_t persist_sync_words(int L) { return (size_t)L * SL + 1; }
 
@@ -1003,6 +1120,8 @@ void launch_decode_step(const PkArgs& a, hipStream_t s) {
   const char* e = getenv("MS_PK_SPIN");
   PkArgs b = a;
   b.spin = e ? (unsigned)strtoul(e, nullptr, 10) : (1u << 19);
+  const char* dv = getenv("MS_PK_DEPTH");  // DMA instructions in flight per loader wave (tuning)
+  b.depth = dv ? std::max(4, std::min(44, atoi(dv))) : DEPTH;
   static unsigned long long* stamps = [] {
     const char* e = getenv("MS_PK_STAMPS");
     void* p = nullptr;

@@ -298,6 +298,7 @@ struct PkLayer {
   const f16_t* g_next;  // the next layer's attn_norm, or the final norm
   f16_t* kc;            // this layer's K / V pools (slot-major pages)
   f16_t* vc;
+  const char* packed;   // the layer's matrices in stream order (launch_pack_layer)
 };
 
 struct PkArgs {
@@ -323,11 +324,17 @@ struct PkArgs {
   unsigned* err;   // set on a hand-off timeout (never cleared here)
   unsigned spin;   // global polls before a hand-off gives up (MS_PK_SPIN; tests force 0)
   unsigned long long* stamps;  // diagnostic timeline (MS_PK_STAMPS=1): [256][L][16] s_memrealtime
+  int depth;                   // DMA instructions each loader wave keeps in flight (MS_PK_DEPTH)
 };
 // the persistent step's in-kernel timeline of its latest launch (MS_PK_STAMPS=1), [256][L][16]
 void persist_stamps(unsigned long long* host, int n);
 
 size_t persist_sync_words(int L);
+// the layer's QKV / O / gate-up / down weights in the persistent step's stream order (every ring slot
+// contiguous, LDS swizzle applied): persist_packed_bytes_per_layer() bytes per layer
+size_t persist_packed_bytes_per_layer();
+void launch_pack_layer(const f16_t* wqkv, const f16_t* wo, const f16_t* wgu, const f16_t* wdown, void* out,
+                       hipStream_t s);
 bool persist_supported(int max_batch, int H, int F, int Hq, int Hk, int Dh, int L, int ppb, int n_cu);
 void launch_decode_step(const PkArgs& a, hipStream_t s);
 

@@ -11,6 +11,7 @@ import os
 import sys
 
 os.environ["MS_PK_STAMPS"] = "1"
+os.environ.setdefault("MS_PERSIST", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "map-reduced-approach-for-vietnamese-long-document-summarization_amd"))
@@ -59,6 +60,18 @@ def main():
               f"med {np.nanmedian(np.nanmedian(v, axis=0)):8.2f}  max {np.nanmedian(np.nanmax(v, axis=0)):8.2f}")
     if a.layers > 5:
         trace(tr, s[0, 5, 0])
+        # the slowest attention items of layer 5: (cu, split, seq, kv head) and their stamps
+        r5 = rel[:, 5]
+        order = np.argsort(-r5[:, 9])
+        print("slowest merges, layer 5: cu s b g | gather prologue merge  (us)")
+        for cu in order[:12]:
+            print(f"  {cu:3d} {cu // 64} {(cu % 64) // 8} {cu % 8} | {r5[cu, 2]:7.2f} {r5[cu, 8]:7.2f} {r5[cu, 9]:7.2f}")
+        print("fastest merges:")
+        for cu in order[-6:]:
+            print(f"  {cu:3d} {cu // 64} {(cu % 64) // 8} {cu % 8} | {r5[cu, 2]:7.2f} {r5[cu, 8]:7.2f} {r5[cu, 9]:7.2f}")
+        for sp in range(4):
+            sel = [cu for cu in range(256) if cu // 64 == sp]
+            print(f"split {sp}: merge median {np.median(r5[sel, 9]):.2f} max {np.max(r5[sel, 9]):.2f}")
 
 
 def trace(tr, t0):
