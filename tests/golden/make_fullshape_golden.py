@@ -55,10 +55,11 @@ for p in (ROOT, PKG, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-MODEL = {"flat": (0, 0.02, 0.0), "sharp": (77, 0.02, 0.1), "q4km": (2, 0.02, 0.0)}  # seed, std, norm jitter
+MODEL = {"flat": (0, 0.02, 0.0), "sharp": (77, 0.02, 0.1), "q4km": (2, 0.02, 0.0),
+         "sharpq4km": (2, 0.02, 0.0)}  # seed, std, norm jitter
 P, GEN, TOPK = 2048, 128, 16
 SKETCH_SEED = 1234
-CHUNKS = {"flat": (0, 5), "sharp": (0, 3), "q4km": (0, 5)}
+CHUNKS = {"flat": (0, 5), "sharp": (0, 3), "q4km": (0, 5), "sharpq4km": (0, 3)}
 
 
 def sketch_mats(H, V):
@@ -91,7 +92,7 @@ def topk(v, k=TOPK):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--which", choices=("flat", "sharp", "q4km"), required=True)
+    ap.add_argument("--which", choices=("flat", "sharp", "q4km", "sharpq4km"), required=True)
     ap.add_argument("--mode", choices=("fp32", "f16", "engine"), required=True)
     ap.add_argument("--gen", type=int, default=GEN)
     ap.add_argument("--out", default=None)
@@ -108,6 +109,11 @@ def main():
         # dequantisation (oracle/synth.py restates the device block generator bit for bit)
         from oracle.synth import make_q4km_blocks, q4km_weights
         w = q4km_weights(cfg, make_q4km_blocks(cfg, SEED, STD), SEED, JIT)
+    elif args.which == "sharpq4km":
+        # the copy head on the Q4_K_M model: quantised overrides (tests/golden/sharp_model.py
+        # q4km_overrides), every block at its exact fp32 dequantisation
+        import sharp_model
+        _, w = sharp_model.q4km_model(cfg)
     else:
         w = make_weights(cfg, SEED, std=STD, jitter=JIT)
     meta = {"model": cfg.name, "n_layers": cfg.n_layers, "seed": SEED, "std": STD, "jitter": JIT,
@@ -116,6 +122,10 @@ def main():
             "chunks": list(CHUNKS[args.which]), "sketch_seed": SKETCH_SEED,
             "generator": "tests/golden/make_fullshape_golden.py (oracle/llama_ref.py, numpy "
                          + np.__version__ + ")"}
+    if args.which == "sharpq4km":
+        import sharp_model
+        meta.update(copy_offset=sharp_model.COPY_OFFSET, design_seed=sharp_model.DESIGN_SEED,
+                    copy_layer=sharp_model.COPY_LAYER, c_layer=sharp_model.C_LAYER_Q4KM)
     if args.which == "sharp":
         import sharp_model
         w = sharp_model.apply(w, sharp_model.copy_head_overrides(cfg, SEED, JIT))

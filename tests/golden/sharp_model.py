@@ -36,7 +36,11 @@ import math
 
 import numpy as np
 
-from oracle.llama_ref import rope_inv_freq
+import os as _os
+import sys as _sys
+
+_sys.path.insert(0, _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))))
+from oracle.llama_ref import rope_inv_freq  # noqa: E402
 from oracle.synth import ATTN_NORM, bf16_rne, norm
 
 COPY_OFFSET = 36
@@ -96,6 +100,69 @@ def apply(weights: dict, ov: dict) -> dict:
     return weights
 
 
+# ---- the same copy head on Q4_K_M weights (configs[4])
+# base: bench.py's Q4_K_M model (ms_init_synthetic_q seed 2, oracle/synth.py make_q4km_blocks);
+# the embedding (tied lm_head, Q6_K in the mix) and layer COPY_LAYER's Wq / Wk / Wv / Wo are
+# replaced by QUANTISED copies of the overrides above (oracle/quantize.py; each tensor in its
+# Q4_K_M type), and the oracle runs the EXACT fp32 dequantisation of every block -- the engine
+# runs the blocks through its dequant-fused GEMVs / Q6_K lm_head.
+Q4KM_SEED = 2
+# u_hat . (rmsnorm(x) * g) at layer COPY_LAYER's input on the Q4_K_M base (calibrate_q4km())
+C_LAYER_Q4KM = 45.477
+
+
+def q4km_overrides(cfg, c_layer: float = None) -> dict:
+    """{"embed" | (COPY_LAYER, name): (ggml type, blocks uint8 [n][bytes])} of the copy head."""
+    from oracle.quantize import quantize
+    from oracle.quants import q4_k_m_type
+    c = C_LAYER_Q4KM if c_layer is None else c_layer
+    ov = copy_head_overrides(cfg, Q4KM_SEED, 0.0, c_layer=c)
+    t = q4_k_m_type("embed", 0, cfg.n_layers)
+    out = {"embed": (t, quantize(ov["embed"], t))}
+    for name in ("wq", "wk", "wv", "wo"):
+        t = q4_k_m_type(name, COPY_LAYER, cfg.n_layers)
+        out[(COPY_LAYER, name)] = (t, quantize(ov[name], t))
+    return out
+
+
+def q4km_model(cfg, c_layer: float = None):
+    """(blocks dict as oracle/synth.py make_q4km_blocks, oracle float weights at the exact
+    dequantisation) of the sharp Q4_K_M model."""
+    from oracle.synth import make_q4km_blocks, q4km_weights
+    qw = make_q4km_blocks(cfg, Q4KM_SEED, 0.02)
+    qw.update(q4km_overrides(cfg, c_layer))
+    return qw, q4km_weights(cfg, qw, Q4KM_SEED, 0.0)
+
+
+def calibrate_q4km(n_tok: int = 256):
+    """Design step (CPU, a few min): C_LAYER_Q4KM on the Q4_K_M base, then the copy-rule check."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.join(root, "map-reduced-approach-for-vietnamese-long-document-summarization_amd"))
+    from mapsum.config import LLAMA32_3B as cfg
+    from oracle.llama_ref import OracleLlama, rms_rinv
+    _, w = q4km_model(cfg, c_layer=1.0)
+    prompt = np.random.default_rng(5).integers(0, 128000, n_tok)
+    _, probes = OracleLlama(cfg, w, mode="fp32").forward(prompt, collect=True)
+    x = probes[COPY_LAYER - 1]
+    _, uh = _embedding(cfg, np.random.default_rng(DESIGN_SEED))
+    g = w["layers"][COPY_LAYER]["attn_norm"]
+    c = float(np.mean((x * rms_rinv(x, cfg.norm_eps) * g) @ uh))
+    print(f"C_LAYER_Q4KM = {c:.3f} (module constant {C_LAYER_Q4KM})", flush=True)
+    del w, probes
+    _, w = q4km_model(cfg, c_layer=c)
+    lg, _ = OracleLlama(cfg, w, mode="fp32").forward(prompt, all_logits=True)
+    pos = np.arange(COPY_OFFSET + 8, n_tok)
+    top = np.argsort(-lg[pos], 1)[:, :2]
+    ok = np.mean(top[:, 0] == prompt[pos - COPY_OFFSET])
+    gap = lg[pos, top[:, 0]] - lg[pos, top[:, 1]]
+    rel_gap = gap / np.sqrt(np.mean(lg[pos] ** 2, 1))
+    print(f"copy rule at {ok:.4f} of {len(pos)} positions; top-2 gap min {gap.min():.2f} median "
+          f"{np.median(gap):.2f} (min {rel_gap.min():.2f} logit rms)")
+    return c
+
+
 def expected_continuation(prompt, n: int) -> list:
     """The copy head's greedy continuation: token(p+1) = token(p - COPY_OFFSET)."""
     seq = [int(t) for t in prompt]
@@ -137,4 +204,5 @@ def calibrate(seed: int = 77, jitter: float = 0.1, n_tok: int = 256):
 
 
 if __name__ == "__main__":
-    calibrate()
+    import sys as _sys
+    calibrate_q4km() if "--q4km" in _sys.argv else calibrate()

@@ -432,6 +432,7 @@ def test_config2_continuous_batching_full_width(oracle):
         e.close()
 
 
+@pytest.mark.parametrize("slots", [NCHUNK, 32])
 def test_decode_tail_bit_exact(dev, chunks, monkeypatch, slots):
     """The one-launch decode step tail (k_misc.hip decode_tail_kernel: the lm_head partials'
     argmax, the chained-step advance with its last-arrival step ticket, the next step's

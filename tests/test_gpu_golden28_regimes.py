@@ -37,12 +37,17 @@ torch = pytest.importorskip("torch")
 from test_gpu_golden28 import (CFG, DECISIVE, GOLD, TOL, _engine, _near_tie, load_fixture,  # noqa: E402
                                rel, sketch_mats)
 
+from mapsum import _lib as L  # noqa: E402
 from mapsum.engine import Engine  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(8, "q4km"), (128, "q4km")]
-CASES = [(s, w, ci) for s, w in RUNS for ci in ((0, 3) if w == "sharp" else (0, 5))]
+# sharpq4km: the copy head on the Q4_K_M weights, quantised into K-quant
+# blocks (tests/golden/sharp_model.py q4km_overrides) -- the decisive greedy bar on K-quant weights
+RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(8, "q4km"), (128, "q4km")] + \
+    [(8, "sharpq4km"), (128, "sharpq4km")]
+CASES = [(s, w, ci) for s, w in RUNS for ci in ((0, 3) if w in ("sharp", "sharpq4km") else (0, 5))]
 _CACHE = {}
+_OVERRIDES = {}
 
 
 def _bench():
@@ -52,10 +57,25 @@ def _bench():
     return bench
 
 
-def _q4km_engine(meta, slots):
+def _q4km_engine(meta, slots, sharp=False):
     e = Engine(CFG, device=0, max_batch=slots, max_ctx=meta["prompt_len"] + 256,
                max_prefill_tokens=8 * meta["prompt_len"])
     e.init_synthetic_q(seed=meta["seed"], scale=meta["std"], norm_jitter=meta["jitter"])
+    if sharp:
+        # the copy head's quantised blocks over the synthetic Q4_K_M model (the fixture's oracle ran
+        # the exact dequantisation of these same bytes)
+        import sys
+        sys.path.insert(0, os.path.join(HERE, "golden"))
+        import sharp_model
+        assert meta["copy_layer"] == sharp_model.COPY_LAYER and meta["c_layer"] == sharp_model.C_LAYER_Q4KM
+        if "ov" not in _OVERRIDES:  # ~30 s of numpy quantisation, shared by the 8- and 128-slot engines
+            _OVERRIDES["ov"] = sharp_model.q4km_overrides(CFG)
+        ov = _OVERRIDES["ov"]
+        qt, blocks = ov["embed"]
+        e.load_tensor_q(L.MS_T_EMBED, 0, qt, blocks.reshape(-1))
+        for name, t in (("wq", L.MS_T_WQ), ("wk", L.MS_T_WK), ("wv", L.MS_T_WV), ("wo", L.MS_T_WO)):
+            qt, blocks = ov[(sharp_model.COPY_LAYER, name)]
+            e.load_tensor_q(t, sharp_model.COPY_LAYER, qt, blocks.reshape(-1))
     return e
 
 
@@ -65,7 +85,8 @@ def _run(slots, which):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     meta, d = load_fixture(which, "fp32")
-    eng = _q4km_engine(meta, slots) if which == "q4km" else _engine(meta, which, max_batch=slots)
+    eng = (_q4km_engine(meta, slots, sharp=which == "sharpq4km") if which in ("q4km", "sharpq4km")
+           else _engine(meta, which, max_batch=slots))
     R, Rv = sketch_mats()
     out = {"layers": {}, "logits": {}, "forced": {}, "free": {}}
     try:
@@ -156,7 +177,7 @@ def test_regime_teacher_forced_decode(slots, which, ci):
     for i in flips:
         assert _near_tie(ti[i], tv[i], got[i]), (i, got[i], ti[i, :3], tv[i, :3])
     assert np.mean(got[dec] == ref[dec]) >= 0.99
-    if which == "sharp":
+    if which in ("sharp", "sharpq4km"):
         assert np.array_equal(got, ref)
 
 
@@ -172,8 +193,8 @@ def test_regime_free_running_greedy(slots, which, ci):
     pre = int(np.argmin(np.append(got[:n] == ref[:n], False)))
     print(f"{slots} slots {which} c{ci} vs fp32: free-running greedy {match:.4f} of the first {n} equal, "
           f"common prefix {pre}")
-    if which == "sharp":
-        assert match >= 0.99  # BASELINE.json north_star, literally
+    if which in ("sharp", "sharpq4km"):
+        assert match >= 0.99  # BASELINE.json north_star, literally (fp16 and Q4_K_M weights)
     elif pre < n:
         assert _near_tie(d[k + "gen_top_ids"][pre], d[k + "gen_top_vals"][pre], got[pre]), \
             (pre, got[pre], d[k + "gen_top_ids"][pre, :3], d[k + "gen_top_vals"][pre, :3])

@@ -101,3 +101,18 @@ def test_random_blocks_statistics_and_mix():
     types = [Q.q4_k_m_type("wv", i, 28) for i in range(28)]
     assert types.count(Q.GGML_TYPE_Q6_K) >= 8 and types.count(Q.GGML_TYPE_Q4_K) >= 8
     assert Q.q4_k_m_type("embed", 0, 28) == Q.GGML_TYPE_Q6_K
+
+
+@pytest.mark.parametrize("qtype,tol", [(Q.GGML_TYPE_Q4_K, 0.10), (Q.GGML_TYPE_Q6_K, 0.03)])
+def test_quantizer_writes_blocks_the_dequantiser_reads(qtype, tol):
+    """oracle/quantize.py (the K-quant fixtures' writer): its blocks dequantise (ggml's C
+    restatement) back to the input within the format's error, and re-quantising the
+    dequantised weights reproduces them (a fixed point of quantize o dequant)."""
+    from oracle.quantize import quantize
+    x = np.random.default_rng(3).standard_normal(64 * 256).astype(np.float32) * 0.02
+    b = quantize(x, qtype)
+    y = Q.c_dequant(b, qtype)
+    assert np.array_equal(y, Q.dequant(b, qtype))
+    assert np.linalg.norm(y - x) / np.linalg.norm(x) < tol
+    y2 = Q.c_dequant(quantize(y, qtype), qtype)
+    assert np.linalg.norm(y2 - y) / np.linalg.norm(y) < tol / 4
