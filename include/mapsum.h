@@ -316,6 +316,13 @@ int ms_op_qgemv(const void* X, int32_t ggml_type, const void* packed_rows, void*
    (the quantised counterpart of ms_op_gemv_split; K % (256*S) == 0) */
 int ms_op_qgemv_split(const void* X, int32_t ggml_type, const void* packed_rows, float* slabs,
                       int32_t M, int32_t N, int32_t K, int32_t S, void* stream);
+/* large-batch K-quant decode GEMM (M <= 256 rows): ms_op_dgemm over the packed rows, each weight
+   dequantised in registers to its fp16-copy value f16(ggml dequant); epilogues MS_EPI_STORE_F32
+   (S > 1: split-K slabs [S][M][N]), MS_EPI_SWIGLU, MS_EPI_ARGMAX; N % 64 == 0, K % (256 S) == 0
+   with K / (256 S) even or a multiple of 3 (the engine's K-quant decode projections in engines
+   of >= 65 slots) */
+int ms_op_qdgemm(const void* X, int32_t ggml_type, const void* packed_rows, void* out, int32_t M,
+                 int32_t N, int32_t K, int32_t S, int32_t ldo, int32_t epilogue, void* stream);
 /* the input of a normalised projection: y fp16 [rows][hidden] = f16(x * w * 2^-4) and ssq[r] = sum
    of x[r]^2 over x fp32 [.][hidden] rows (row_idx optional gather); the projection then scales
    its output rows by 16/sqrt(ssq / hidden + eps) (ms_op_set_row_scale).  The 2^-4 pre-scale

@@ -223,10 +223,20 @@ struct ms_engine {
     if (has_quant && !qresid_ok) return false;
     return !(q && q->ready()) || qresid;
   }
-  // the large-batch arithmetic (skinny GEMM on the fp16 weights) for engines of >= dgemm_min
-  // slots -- except engines with K-quant weights: they keep the exact Q4_K / Q6_K GEMV at every
-  // batch size, in row groups of <= kMaxGemvRows (a row's sum order does not depend on its group)
-  bool large(int) const { return large_engine && !has_quant; }
+  // the large-batch arithmetic (skinny GEMM) for engines of >= dgemm_min slots.  Engines with
+  // K-quant weights keep the exact Q4_K / Q6_K GEMV up to qlarge_min - 1 slots (in row groups of
+  // <= kMaxGemvRows above 64: a row's sum order does not depend on its group); from qlarge_min
+  // (MS_QLARGE_MIN, default 65: the row groups' weight re-streams cost Q4_K_M 18.2 ms per decode
+  // step at 128 slots, profiles/r06/v9_*) they take the large regime too, where every quantised
+  // matrix streams its packed blocks once per step through the K-quant skinny GEMM
+  // (k_qdgemm.hip, the fp16-copy values; MS_QDGEMM=0: the fp16 copies through k_dgemm.hip)
+  int qlarge_min = 65;
+  bool qdgemm_on = true;
+  bool large(int) const { return large_engine && (!has_quant || cfg.max_batch >= qlarge_min); }
+  // the K-quant skinny GEMM for this matrix (large regime)
+  bool qd(const QSlot* q, int M, int N, int K, int S, int epi) const {
+    return qdgemm_on && q && q->ready() && qdgemm_supported(M, N, K, S, epi, q->m);
+  }
   bool row_groups(int B) const { return !large(B) && B > kMaxGemvRows; }
   // split count of every quantised slab projection (MS_QSPLIT; 0: as fp16): 4 measured best
   // for Q4_K_M at B = 8 -- 1.878 vs 1.900 ms/step with the fp16 splits (6 / 6 / 4), 2 / 3 / 8
@@ -455,9 +465,12 @@ struct ms_engine {
     if (rs) ga.rs = *rs;
     ga.slab_rows = slab_rows;
     int used = 1;
-    if (large(M)) {  // skinny GEMM on the fp16 weights (K-quant copies included)
-      launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1,
-                   M <= 128 && N % 128 == 0 ? dwn : 4);
+    if (large(M)) {  // skinny GEMM: the packed K-quant blocks, or the fp16 weights
+      if (qd(q, M, N, K, Sl, MS_GEMV_EPI_STORE_F32))
+        launch_qdgemm(X, q->m, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
+      else
+        launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1,
+                     M <= 128 && N % 128 == 0 ? dwn : 4);
       used = Sl;
     } else if (q && q->ready() && qgemv_supported(M, N, K, MS_GEMV_EPI_STORE_F32)) {
       // Q4_K/Q6_K: same split-K as fp16 (a 16-row tile carries 3.6x fewer weight bytes, so
@@ -546,7 +559,10 @@ struct ms_engine {
       // gate/up + SwiGLU on the skinny GEMM (41 vs 55 us for the 128x128 GEMM at M = 128,
       // profiles/r02/v7_dgemm_lds_sync_ab.txt; fused_decode checked M <= 256)
       prof_begin(K_GEMV);
-      launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn, dgemm_kh);
+      if (qd(&Q[QS_GU], B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU))
+        launch_qdgemm(xb, Q[QS_GU].m, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn);
+      else
+        launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn, dgemm_kh);
       prof_end(K_GEMV);
     } else {
       GemvArgs gg{};
@@ -863,6 +879,8 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_SPLIT_DOWN")) E.split_down = atoi(v);
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
+    if (const char* v = getenv("MS_QLARGE_MIN")) E.qlarge_min = atoi(v);
+    if (const char* v = getenv("MS_QDGEMM")) E.qdgemm_on = atoi(v) != 0;
     // (the k-half block steps 128 k at a time: hidden sizes that are not a multiple of 128
     // keep the 4-wave block)
     E.dgemm_kh = cfg->max_batch <= 128 && E.H % 128 == 0 ? dgemm_kh_setting() : 1;
@@ -1518,8 +1536,11 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     E.prof_begin(K_LMHEAD);
     // no row scale: r > 0 keeps every row's order (the logits themselves are never stored)
     // 4-wave blocks always: a 2004-block grid keeps two per CU (k_dgemm.hip kh)
-    launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1,
-                 B <= 128 && E.V % 128 == 0 ? E.dwn_lm : 4);
+    if (E.qd(&E.lmq, B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX))
+      launch_qdgemm(E.xb, E.lmq.m, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr);
+    else
+      launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1,
+                   B <= 128 && E.V % 128 == 0 ? E.dwn_lm : 4);
     E.prof_end(K_LMHEAD);
     decode_tail(E, B, d, tiles);
     return;
@@ -2159,6 +2180,25 @@ int ms_op_qgemv_split(const void* X, int32_t type, const void* packed, float* sl
     q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
     GemvArgs ga;
     launch_qgemv_split((const f16_t*)X, q, slabs, M, N, K, S, (hipStream_t)stream, op_gemv_args(ga));
+  });
+}
+
+int ms_op_qdgemm(const void* X, int32_t type, const void* packed, void* out, int32_t M, int32_t N, int32_t K,
+                 int32_t S, int32_t ldo, int32_t epi, void* stream) {
+  return op_guard([&] {
+    REQUIRE(X && packed && out && N >= 64 && K >= 256 && S >= 1, MS_EINVAL, "bad qdgemm operands");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "qdgemm row scale: one-tile statistics only");
+    QMat q{};
+    q.n = 1;
+    q.base0 = (const uint8_t*)packed;
+    q.row0_0 = 0;
+    q.type0 = type;
+    q.row_bytes0 = (K / 256) * qblock_bytes(type, true);
+    const int e = epi == MS_EPI_ARGMAX ? MS_GEMV_EPI_ARGMAX : epi;
+    REQUIRE(qdgemm_supported(M, N, K, S, e, q), MS_EINVAL,
+            "qdgemm shape unsupported (M <= 256, N % 64 == 0, K % (256 S) == 0, S > 1 only for fp32 slabs)");
+    launch_qdgemm((const f16_t*)X, q, out, M, N, K, S, ldo, e, (hipStream_t)stream, &g_op_rs);
   });
 }
 

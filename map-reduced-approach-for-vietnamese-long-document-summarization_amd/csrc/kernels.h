@@ -225,6 +225,14 @@ struct QMat {
   const uint8_t* base1; int row0_1, type1, row_bytes1;
   const uint8_t* base2; int row0_2, type2, row_bytes2;
 };
+// large-batch K-quant decode projections (k_qdgemm.hip): the skinny GEMM with the weights
+// streamed as packed Q4_K / Q6_K rows and dequantised in registers to their fp16-copy values;
+// each region launched on its own (rows % 64 == 0 per region, first region at row 0), SwiGLU /
+// argmax need one region; S > 1 = fp32 split-K slabs; K % (256 S) == 0, M <= 256
+bool qdgemm_supported(int M, int N, int K, int S, int epi, const QMat& q);
+void launch_qdgemm(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int S, int ldo, int epi,
+                   hipStream_t s, const RowScale* rs = nullptr);
+
 inline uint64_t smix_host(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

@@ -30,7 +30,7 @@ MS_DBG_KPOOL, MS_DBG_VPOOL, MS_DBG_DECODE_LOGITS, MS_DBG_DECODE_X = range(4)
 
 EXPORTED = (
     "ms_create", "ms_destroy", "ms_last_error", "ms_load_weight", "ms_init_synthetic",
-    "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv", "ms_op_qgemv_split",
+    "ms_load_weight_q", "ms_init_synthetic_q", "ms_op_dequant", "ms_op_quant_rows", "ms_op_qgemv", "ms_op_qgemv_split", "ms_op_qdgemm",
     "ms_submit", "ms_step", "ms_poll", "ms_pending", "ms_get_stats", "ms_reset_stats",
     "ms_set_profiling", "ms_synchronize", "ms_forward", "ms_op_gemm", "ms_op_gemv_workspace",
     "ms_op_gemv", "ms_op_gemv_tuned", "ms_op_gemv_split", "ms_op_dgemm", "ms_op_residual_rmsnorm", "ms_op_rmsnorm",
@@ -102,6 +102,7 @@ def load_at(path: str, ab: bool = True) -> C.CDLL:
         "ms_op_quant_rows": (i32, [i32, vp, i32, i32, vp, vp, vp]),
         "ms_op_qgemv": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, vp]),
         "ms_op_qgemv_split": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, vp]),
+        "ms_op_qdgemm": (i32, [vp, i32, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
         "ms_submit": (i32, [vp, pi32, i32, i32, u32, u64]),
         "ms_step": (i32, [vp]),
         "ms_poll": (i32, [vp, C.POINTER(MsResult), i32]),

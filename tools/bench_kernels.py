@@ -190,6 +190,60 @@ def bench_qgemv(lib, M):
         print(line, flush=True)
 
 
+
+def bench_qdgemm(lib, ms=(64, 128, 256), only=None):
+    """Large-batch K-quant decode GEMM (k_qdgemm.hip) against the fp16 skinny GEMM (k_dgemm.hip)
+    on the same shapes, > 512 MB rotations of packed / fp16 weights (no MALL reuse).
+    GB/s = the weight bytes each reads / time."""
+    from oracle import quants as Q
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, N, K, qt, epi, splits in [("qkv", 5120, 3072, 12, 3, (1, 2, 3, 6)), ("o", 3072, 3072, 12, 3, (1, 2, 4)),
+                                        ("gu", 16384, 3072, 12, 2, (1,)), ("down", 3072, 8192, 12, 3, (1, 2, 4, 8)),
+                                        ("down6", 3072, 8192, 14, 3, (2, 4, 8)), ("lm_head6", 128256, 3072, 14, 5, (1,))]:
+        if only and name not in only:
+            continue
+        bpb = 144 if qt == 12 else 224
+        nbytes = N * (K // 256) * bpb
+        rows_src = min(N, 4096)
+        b = Q.random_blocks(qt, rows_src * K // 256, seed=1, scale=0.02)
+        bd = torch.from_numpy(b.reshape(-1)).to(dev)
+        wbf = torch.empty(rows_src, K, dtype=torch.float16, device=dev)
+        tmp = torch.empty(rows_src * (K // 256) * bpb, dtype=torch.uint8, device=dev)
+        lib.ms_op_quant_rows(qt, bd.data_ptr(), rows_src, K, wbf.data_ptr(), tmp.data_ptr(), st)
+        pks, ws16 = [], []
+        for _ in range(max(2, -(-512 * 2**20 // nbytes))):
+            pk = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            for r0 in range(0, N, rows_src):  # tile the random rows over the matrix
+                rr = min(rows_src, N - r0)
+                pk[r0 * (K // 256) * bpb:(r0 + rr) * (K // 256) * bpb] = tmp[:rr * (K // 256) * bpb]
+            pks.append(pk)
+        for _ in range(max(2, -(-512 * 2**20 // (N * K * 2)))):
+            ws16.append(wbf.repeat((N + rows_src - 1) // rows_src, 1)[:N].contiguous())
+        ldo = N // 2 if epi == 2 else (N // 16 if epi == 5 else N)
+        for M in ms:
+            X = torch.randn(M, K, device=dev).to(torch.float16)
+            out = torch.zeros(8 * M * N, device=dev)
+            i = [0]
+
+            def nxt(lst):
+                i[0] += 1
+                return lst[i[0] % len(lst)]
+            line = f"{name:8s} N={N:6d} K={K:5d} M={M:3d} {nbytes/1e6:6.1f} MB |"
+            for S in splits:
+                e, lo = (epi, ldo) if S == 1 else (3, N)
+                if lib.ms_op_qdgemm(X.data_ptr(), qt, pks[0].data_ptr(), out.data_ptr(), M, N, K, S, lo, e, st):
+                    line += f" q S{S} n/a |"
+                else:
+                    t = timeit(lambda: lib.ms_op_qdgemm(X.data_ptr(), qt, nxt(pks).data_ptr(), out.data_ptr(), M, N, K,
+                                                        S, lo, e, st))
+                    line += f" q S{S} {t*1e3:6.1f}us {nbytes/t/1e6:5.0f} |"
+                if lib.ms_op_dgemm(X.data_ptr(), ws16[0].data_ptr(), out.data_ptr(), M, N, K, S, lo, e, st) == 0:
+                    t = timeit(lambda: lib.ms_op_dgemm(X.data_ptr(), nxt(ws16).data_ptr(), out.data_ptr(), M, N, K, S,
+                                                       lo, e, st))
+                    line += f" f16 {t*1e3:6.1f}us |"
+            print(line, flush=True)
+
 def bench_camp(lib, M):
     """Unsplit decode GEMV over weight rows padded to ldk = K + pad elements: does the row
     stride (16 KB for the down projection) concentrate a launch on a few HBM channels?"""
@@ -305,7 +359,7 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=Fa
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp", "qdgemm"])
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--ascale", type=float, default=1.0, help="gemm: scale of the uniform A entries")
     ap.add_argument("--trunc", type=int, default=0, help="gemm: clear this many low mantissa bits of A and W")
@@ -315,6 +369,8 @@ if __name__ == "__main__":
     ap.add_argument("--ref-lib", default="", help="gemm: a second build (e.g. libmapsum_base.so) timed and compared")
     ap.add_argument("--resid", action="store_true", help="gemm: O / down through ms_op_gemm_resid (the engine's form)")
     ap.add_argument("--kh", type=int, default=1, help="dgemm: block form (ms_set_dgemm_kh: 1 4-wave, 2 k-half 8-wave)")
+    ap.add_argument("--ms", default="64,128,256", help="qdgemm: batch rows")
+    ap.add_argument("--only", default="", help="qdgemm: comma-separated shape names")
     a = ap.parse_args()
     lib = L.load()
     if a.what == "gemv":
@@ -330,6 +386,8 @@ if __name__ == "__main__":
         bench_qgemv(lib, a.m)
     elif a.what == "camp":
         bench_camp(lib, a.m)
+    elif a.what == "qdgemm":
+        bench_qdgemm(lib, tuple(int(v) for v in a.ms.split(",")), a.only.split(",") if a.only else None)
     else:
         ref = L.load_at(a.ref_lib) if a.ref_lib else None
         bench_gemm(lib, a.rs, tuple(int(v) for v in a.variants.split(",")), a.ascale, a.trunc, a.torch, ref, a.resid)
