@@ -229,13 +229,19 @@ struct ms_engine {
   // (MS_QLARGE_MIN, default 65: the row groups' weight re-streams cost Q4_K_M 18.2 ms per decode
   // step at 128 slots, profiles/r06/v9_*) they take the large regime too, where every quantised
   // matrix streams its packed blocks once per step through the K-quant skinny GEMM
-  // (k_qdgemm.hip, the fp16-copy values; MS_QDGEMM=0: the fp16 copies through k_dgemm.hip)
+  // (k_qdgemm.hip, the fp16-copy values).  MS_QDGEMM selects which matrices: 1 (default) the
+  // all-Q4_K ones -- a Q6_K matrix (the Q4_K_M lm_head, half of the down / V projections) runs
+  // its fp16 copy through k_dgemm.hip, which measured faster there (its dequant is twice the
+  // VALU; r06/v11_*) --, 2 every K-quant matrix, 0 none (the fp16 copies everywhere)
   int qlarge_min = 65;
-  bool qdgemm_on = true;
+  int qdgemm_mode = 1;
   bool large(int) const { return large_engine && (!has_quant || cfg.max_batch >= qlarge_min); }
   // the K-quant skinny GEMM for this matrix (large regime)
   bool qd(const QSlot* q, int M, int N, int K, int S, int epi) const {
-    return qdgemm_on && q && q->ready() && qdgemm_supported(M, N, K, S, epi, q->m);
+    if (!qdgemm_mode || !q || !q->ready()) return false;
+    const QMat& m = q->m;
+    const bool q4 = m.type0 == MS_QT_Q4_K && (m.n < 2 || m.type1 == MS_QT_Q4_K) && (m.n < 3 || m.type2 == MS_QT_Q4_K);
+    return (q4 || qdgemm_mode == 2) && qdgemm_supported(M, N, K, S, epi, m);
   }
   bool row_groups(int B) const { return !large(B) && B > kMaxGemvRows; }
   // split count of every quantised slab projection (MS_QSPLIT; 0: as fp16): 4 measured best
@@ -880,7 +886,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     if (const char* v = getenv("MS_DGEMM_MIN")) E.dgemm_min = atoi(v);
     E.large_engine = cfg->max_batch >= E.dgemm_min;
     if (const char* v = getenv("MS_QLARGE_MIN")) E.qlarge_min = atoi(v);
-    if (const char* v = getenv("MS_QDGEMM")) E.qdgemm_on = atoi(v) != 0;
+    if (const char* v = getenv("MS_QDGEMM")) E.qdgemm_mode = atoi(v);
     // (the k-half block steps 128 k at a time: hidden sizes that are not a multiple of 128
     // keep the 4-wave block)
     E.dgemm_kh = cfg->max_batch <= 128 && E.H % 128 == 0 ? dgemm_kh_setting() : 1;
