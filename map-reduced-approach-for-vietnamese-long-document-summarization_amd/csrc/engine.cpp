@@ -2193,8 +2193,14 @@ int ms_op_qdgemm(const void* X, int32_t type, const void* packed, void* out, int
                  int32_t S, int32_t ldo, int32_t epi, void* stream) {
   return op_guard([&] {
     REQUIRE(X && packed && out && N >= 64 && K >= 256 && S >= 1, MS_EINVAL, "bad qdgemm operands");
-    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K, MS_EINVAL, "ggml type must be Q4_K or Q6_K");
+    REQUIRE(type == MS_QT_Q4_K || type == MS_QT_Q6_K || type == 1, MS_EINVAL, "ggml type must be Q4_K, Q6_K or F16");
     REQUIRE(!g_op_rs.ssq || g_op_rs.tiles == 1, MS_EINVAL, "qdgemm row scale: one-tile statistics only");
+    if (type == 1) {  // fp16 rows [N][K] through the same kernel
+      const int e = epi == MS_EPI_ARGMAX ? MS_GEMV_EPI_ARGMAX : epi;
+      REQUIRE(qdgemm_f16_supported(M, N, K, S, e), MS_EINVAL, "qdgemm (fp16 rows) shape unsupported");
+      launch_qdgemm_f16((const f16_t*)X, (const f16_t*)packed, out, M, N, K, S, ldo, e, (hipStream_t)stream, &g_op_rs);
+      return;
+    }
     QMat q{};
     q.n = 1;
     q.base0 = (const uint8_t*)packed;

@@ -11,9 +11,12 @@
 // profiles/r06/v9_*).  Here each wave dequantises its 16 weight rows ONCE per 32-k MFMA column
 // to fp16 -- the values of the engine's fp16 copy, f16(ggml dequant), the ones every prefill GEMM
 // multiplies -- and feeds all M rows from the block's shared X image with them.
-//  * block: WN waves x 16 weight rows, all M <= 256 rows (MT m-tiles); X register-staged one
-//    64-k step ahead into a double-buffered swizzled LDS image (k_dgemm.hip's scheme, LDS-only
-//    barriers, so the weight loads stay in flight across them);
+//  * block: 4 waves x 16 weight rows, all M <= 256 rows (MT m-tiles); X staged by LDS DMA into a
+//    4-stage swizzled image three 64-k steps ahead, with counted vmcnt waits and fence-free step
+//    barriers, so the weight ring and the later stages stay in flight across them (the time per
+//    step grows with the X bytes every block re-reads -- the bound, not the weight bytes: the
+//    same kernel on fp16 rows, kQdF16, runs gate/up at M = 128 in 33.7 us against 29.0 us on
+//    Q4_K; profiles/r06/v10_*);
 //  * W: one super-block (256 k) of the wave's 16 rows per ring slot, DPF super-blocks in flight
 //    (Q4_K: header + sub-blocks 0-3 / 4-7, 48 B per lane; Q6_K: four 8-B ql pieces, two 8-B qh
 //    pieces, the scales and d);
@@ -26,8 +29,6 @@
 //  * epilogues as the skinny GEMM: fp32 split-K slabs (gridDim.y), SwiGLU on the 16-row
 //    interleaved gate/up rows, greedy argmax partials; the rows' deferred-norm scale.
 // A row's sum order depends only on (K, split), never on M: batch-invariant inside the regime.
-#include <type_traits>
-
 #include "gemv_common.h"
 
 namespace ms {
@@ -46,36 +47,40 @@ struct QdQ6 {  // one packed Q6_K super-block: ql pieces [k4 & 1][n], qh [n], sc
   uint4 sc;
   uint32_t d;
 };
+// fp16 rows through the same kernel (the large regime's fp16 projections): 256 k = 512 B of a row,
+// MFMA column c's 8 weights of lane group g at 64 c + 16 g
+constexpr int kQdF16 = 1;  // ggml_type F16
+struct QdH {
+  uint4 w[8];
+};
 
 __device__ __forceinline__ uint32_t qd_word(const uint4& v, int i) {
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
 
-// QLM: which ql halves (k4 & 1) a Q6_K fetch loads -- a wave group of the k-half form uses one
-// (its MFMA columns share k4's parity); both otherwise.  The loads issued here are exactly the
-// ones the counted waits assume (kQdLoads): none may be left for the compiler to drop.
 // W loads: plain loads the compiler tracks (its own waits cover each ring slot's first use).
 // Every byte a fetch loads is used, so none is dropped or narrowed and each fetch issues exactly
-// kQdLoads instructions -- the counts the step waits assume (checked in the ISA: r06 notes).
+// kQdLoads instructions -- the counts the step waits assume (checked in the ISA).
 __device__ __forceinline__ uint4 qd_ld16(const uint8_t* p) { return ldw16(p); }
 __device__ __forceinline__ uint2 qd_ld8(const uint8_t* p) { return *(const uint2*)p; }
 __device__ __forceinline__ uint32_t qd_ld4(const uint8_t* p) { return *(const uint32_t*)p; }
 
-template <int QLM>
 __device__ __forceinline__ void qd_fetch(QdQ4& r, const uint8_t* bp, int g) {
   r.h = qd_ld16(bp);
   r.q0 = qd_ld16(bp + 16 + 16 * g);
   r.q1 = qd_ld16(bp + 80 + 16 * g);
 }
-template <int QLM>
+__device__ __forceinline__ void qd_fetch(QdH& r, const uint8_t* bp, int g) {
+#pragma unroll
+  for (int c = 0; c < 8; ++c) r.w[c] = qd_ld16(bp + 64 * c + 16 * g);
+}
 __device__ __forceinline__ void qd_fetch(QdQ6& r, const uint8_t* bp, int g) {
   // packed 224-B block (quant_rows_kernel): raw ql[n*64 + half*32 + l] at half*64 + 32n + 8g + i
   // for l = 8g + i; qh and the scales unmoved
 #pragma unroll
   for (int h = 0; h < 2; ++h)
-    if ((QLM >> h) & 1)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) r.ql[h][n] = qd_ld8(bp + h * 64 + 32 * n + 8 * g);
+    for (int n = 0; n < 2; ++n) r.ql[h][n] = qd_ld8(bp + h * 64 + 32 * n + 8 * g);
 #pragma unroll
   for (int n = 0; n < 2; ++n) r.qh[n] = qd_ld8(bp + 128 + 32 * n + 8 * g);
   r.sc = qd_ld16(bp + 192);
@@ -106,6 +111,10 @@ __device__ __forceinline__ f16x8 qd_dequant(const QdQ4& r, int c, int g) {
   qd_deq4(qw & 0x0F0F0F0Fu, d1, -m1, pk[0], pk[1]);
   qd_deq4((qw >> 4) & 0x0F0F0F0Fu, d1, -m1, pk[2], pk[3]);
   return __builtin_bit_cast(f16x8, pk);
+}
+__device__ __forceinline__ f16x8 qd_dequant(const QdH& r, int c, int g) {
+  (void)g;
+  return __builtin_bit_cast(f16x8, r.w[c]);
 }
 __device__ __forceinline__ f16x8 qd_dequant(const QdQ6& r, int c, int g) {
   const int n = c >> 2, k4 = c & 3;  // weights n*128 + k4*32 + l, l = 8g + i
@@ -156,8 +165,8 @@ __device__ __forceinline__ void qd_wait_steady(int q) {
   }
 }
 
-// vector memory instructions of one qd_fetch<QLM>
-template <int QT, int QLM> constexpr int kQdLoads = QT == MS_QT_Q4_K ? 3 : 4 + 2 * ((QLM & 1) + (QLM >> 1));
+// vector memory instructions of one qd_fetch
+template <int QT> constexpr int kQdLoads = QT == MS_QT_Q4_K ? 3 : QT == kQdF16 ? 8 : 8;
 
 // the packed rows of one launch: up to three regions of one type (the fused QKV matrix's Q / K / V
 // allocations), rows [0, r1) in b0, [r1, r2) in b1, [r2, N) in b2 -- each a multiple of 64 rows,
@@ -174,39 +183,34 @@ __device__ __forceinline__ const uint8_t* qd_row(const QdSrc& s, int r) {
 template <int QT> struct QdRegs;
 template <> struct QdRegs<MS_QT_Q4_K> { using T = QdQ4; static constexpr int kBytes = kQ4KBytes; };
 template <> struct QdRegs<MS_QT_Q6_K> { using T = QdQ6; static constexpr int kBytes = kQ6KPacked; };
+template <> struct QdRegs<kQdF16> { using T = QdH; static constexpr int kBytes = 512; };
 
 // DPF: super-blocks of W in flight per wave, a divisor of the split's super-block count (the
 // ring loop then has no early exit, whose merged paths made the compiler drain vmcnt at the
-// loop head).  NT weight tiles of 16 rows per wave: each X fragment read from LDS feeds NT
-// MFMAs.  KH = 2: the block's wave groups take the even / odd MFMA columns of every step (the
-// same X stage, the same weight rows), summed once at the end.
-template <int MT, int EPI, int WN, int QT, int DPF, int KH, int NT>
-__global__ __launch_bounds__(64 * WN * KH) __attribute__((amdgpu_waves_per_eu(MT >= 16 || NT > 1 ? 1 : 2, 2))) void qdgemm_kernel(const f16_t* __restrict__ X,
-                                                                          QdSrc src,
-                                                                          void* __restrict__ out, int M, int N, int K,
-                                                                          int ldk, int ldo, RowScale rs) {
+// loop head).  4 waves x 16 weight rows per block.
+template <int MT, int EPI, int QT, int DPF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MT >= 16 ? 1 : 2, 2))) void qdgemm_kernel(
+    const f16_t* __restrict__ X, QdSrc src, void* __restrict__ out, int M, int N, int K, int ldk, int ldo,
+    RowScale rs) {
   using R = QdRegs<QT>;
-  // vector memory instructions of one W fetch inside the step loop (a k-half wave group loads one
-  // ql half of its Q6_K blocks)
-  constexpr int WF = NT * kQdLoads<QT, KH == 2 ? 1 : 3>;
-  constexpr int NW = WN * KH;                                   // waves
-  constexpr int XR = 16 * MT < 8 * NW ? 8 * NW : 16 * MT;        // X image rows (a KiB piece per wave at least)
-  constexpr int XB = XR * QBK * 2;                              // one stage: XR rows x 128 B
-  constexpr int PW = XB / 1024 / NW;                            // 1-KiB DMA pieces of a stage per wave
+  constexpr int WN = 4;
+  constexpr int WF = kQdLoads<QT>;                  // vector memory instructions of one W fetch
+  constexpr int XR = 16 * MT < 32 ? 32 : 16 * MT;  // X image rows (a KiB piece per wave at least)
+  constexpr int XB = XR * QBK * 2;                  // one stage: XR rows x 128 B
+  constexpr int PW = XB / 1024 / WN;                // 1-KiB DMA pieces of a stage per wave
   // X stages: three 64-k steps in flight (6 / 8 stages at <= 128 rows measured no faster, and cost
   // the 128-row form its second block per CU)
   constexpr int NS = 4;
-  constexpr int XCH = WN * NT * MT * 256 * 4;  // [WN waves][NT][MT][64 lanes][4] f32: k-half sum, SwiGLU pairing
-  constexpr int SMEM = NS * XB > KH * XCH ? NS * XB : KH * XCH;
-  static_assert(PW >= 1 && PW * NW * 1024 == XB, "X stage pieces");
+  constexpr int XCH = WN * MT * 256 * 4;  // [WN waves][MT][64 lanes][4] f32: SwiGLU pairing
+  constexpr int SMEM = NS * XB > XCH ? NS * XB : XCH;
+  static_assert(PW >= 1 && PW * WN * 1024 == XB, "X stage pieces");
   // every counted wait assumes the wave never has more than vmcnt's 63 memory instructions in
   // flight (the W ring plus the X stages ahead): a saturated counter would release a wait early
-  static_assert(DPF * WF + (4 - 1) * PW <= 63, "vector memory instructions in flight exceed vmcnt");
+  static_assert(DPF * WF + (NS - 1) * PW <= 63, "vector memory instructions in flight exceed vmcnt");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave % WN, kh = wave / WN;  // weight-row group, MFMA column parity
+  const int tid = threadIdx.x, lane = tid & 63, wn = tid >> 6;
   const int fr = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * 16 * WN * NT;  // first weight row of the block, within this region
+  const int n0 = blockIdx.x * 16 * WN;  // first weight row of the block
   const int kb = blockIdx.y * K;        // this split's K range in X rows of length ldk
   if constexpr (EPI == MS_GEMV_EPI_STORE_F32) out = (float*)out + (size_t)blockIdx.y * M * ldo;
   const int nk = K / QBK, nsb = K / 256;
@@ -220,26 +224,18 @@ __global__ __launch_bounds__(64 * WN * KH) __attribute__((amdgpu_waves_per_eu(MT
     const int k0 = kb + min(t, nk - 1) * QBK;  // past the end: clamped re-reads
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
-      const int p = wave + NW * i, C = p * 64 + lane, r = C >> 3, c = C & 7;
+      const int p = wn + WN * i, C = p * 64 + lane, r = C >> 3, c = C & 7;
       __builtin_amdgcn_global_load_lds((const void*)(X + (size_t)min(r, M - 1) * ldk + k0 + ((c ^ (r & 7)) << 3)),
                                        (LDS_AS void*)(smem + st * XB + p * 1024), 16, 0, 0);
     }
   };
-  // tile n of wave wn: rows n0 + 16 (NT wn + n) .. +15 (NT = 2: a gate and an up tile of the same
-  // 16 features, the fused matrix interleaving them by 16 rows)
-  const uint8_t* wrow[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n)
-    wrow[n] = qd_row(src, min(n0 + 16 * (NT * wn + n) + fr, N - 1)) + (size_t)blockIdx.y * nsb * R::kBytes;
-  typename R::T wr[DPF][NT];
-  auto fetch = [&](auto qlm, int slot_sb, typename R::T (&dst)[NT]) {
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
-      qd_fetch<decltype(qlm)::value>(dst[n], wrow[n] + (size_t)min(slot_sb, nsb - 1) * R::kBytes, g);
-  };
+  // this lane's weight row n0 + 16 wn + fr
+  const uint8_t* wrow = qd_row(src, min(n0 + 16 * wn + fr, N - 1)) + (size_t)blockIdx.y * nsb * R::kBytes;
+  typename R::T wr[DPF];
+  auto fetch = [&](int sb, typename R::T& dst) { qd_fetch(dst, wrow + (size_t)min(sb, nsb - 1) * R::kBytes, g); };
   // the W ring first (older than every X stage, so no X wait ever counts it), then X(0..NS-2)
 #pragma unroll
-  for (int p = 0; p < DPF; ++p) fetch(std::integral_constant<int, 3>{}, p, wr[p]);
+  for (int p = 0; p < DPF; ++p) fetch(p, wr[p]);
   qd_order();
 #pragma unroll
   for (int a = 0; a < NS - 1; ++a) dma_x(a, a);
@@ -247,175 +243,116 @@ __global__ __launch_bounds__(64 * WN * KH) __attribute__((amdgpu_waves_per_eu(MT
   __builtin_amdgcn_s_waitcnt(vmcnt_imm((NS - 2) * PW));  // X(0) landed
   qd_barrier();
 
-  f32x4 acc[NT][MT];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n)
-#pragma unroll
-    for (int m = 0; m < MT; ++m) acc[n][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // the step loop with the column parity as a constant (a runtime parity would index the W
-  // registers dynamically: the compiler moves them to scratch)
-  auto steps = [&](auto khc) {
-    constexpr int KHC = decltype(khc)::value;
-    // unrolled by DPF super-blocks so every ring slot is a compile-time register set, and by
-    // the super-block's four 64-k steps so every vmcnt immediate is compile-time; past the end
-    // the loads are clamped re-reads, never branched around
-    // (nsb % DPF == 0: host-checked)
-    for (int j0 = 0; j0 < nsb; j0 += DPF) {
+  // unrolled by DPF super-blocks so every ring slot is a compile-time register set, and by the
+  // super-block's four 64-k steps so every vmcnt immediate is compile-time; past the end the
+  // loads are clamped re-reads, never branched around (nsb % DPF == 0: host-checked)
+  for (int j0 = 0; j0 < nsb; j0 += DPF) {
 #pragma unroll
-      for (int jj = 0; jj < DPF; ++jj) {
-        const int j = j0 + jj;
+    for (int jj = 0; jj < DPF; ++jj) {
+      const int j = j0 + jj;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // step t: X stage t % NS, MFMA columns 2q, 2q + 1
-          const int t = 4 * j + q;
-          const char* xs = smem + (t % NS) * XB;
-          // every X fragment of the step read up front (the step's LDS round trip exposed once, not
-          // once per MFMA); the dequant runs under the reads.  MFMA column c = 2q + h: k 32c + 8g ..
-          f16x8 xf[3 - KH][MT];
+      for (int q = 0; q < 4; ++q) {  // step t: X stage t % NS, MFMA columns 2q, 2q + 1
+        const int t = 4 * j + q;
+        const char* xs = smem + (t % NS) * XB;
+        // every X fragment of the step read up front (the step's LDS round trip exposed once, not
+        // once per MFMA); the dequant runs under the reads.  MFMA column c = 2q + h: k 32c + 8g ..
+        f16x8 xf[2][MT];
 #pragma unroll
-          for (int hh = 0; hh < 3 - KH; ++hh) {
-            const int h = KH == 2 ? KHC : hh;
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-              const int row = m * 16 + fr;
-              xf[hh][m] = *(const f16x8*)(xs + row * 128 + (((4 * h + g) ^ (row & 7)) << 4));
-            }
+          for (int m = 0; m < MT; ++m) {
+            const int row = m * 16 + fr;
+            xf[h][m] = *(const f16x8*)(xs + row * 128 + (((4 * h + g) ^ (row & 7)) << 4));
           }
-          __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int hh = 0; hh < 3 - KH; ++hh)
+        for (int h = 0; h < 2; ++h) {
+          const f16x8 wf = qd_dequant(wr[jj], 2 * q + h, g);
 #pragma unroll
-            for (int n = 0; n < NT; ++n) {
-              const f16x8 wf = qd_dequant(wr[jj][n], 2 * q + (KH == 2 ? KHC : hh), g);
-#pragma unroll
-              for (int m = 0; m < MT; ++m) acc[n][m] = mfma16(xf[hh][m], wf, acc[n][m]);
-            }
-          qd_order();
-          dma_x((t + NS - 1) % NS, t + NS - 1);  // into the stage every wave finished reading in step t - 1
-          qd_order();
-          if (q == 3) fetch(std::integral_constant<int, KH == 2 ? 1 << KHC : 3>{}, j + DPF, wr[jj]);  // slot consumed
-          qd_order();
-          // X(t+1) landed: at most the instructions issued after its DMA pending -- the DMAs of
-          // steps t-NS+3 .. t and the W fetches of steps t-NS+2 .. t (those with s % 4 == 3); before
-          // step NS-2 its DMA came from the prologue (no fetch after it: the fetch-free count waits
-          // at least as long)
-          constexpr int kDmaAfter = (NS - 2) * PW;
-          if (t >= NS - 2)
-            qd_wait_steady<kDmaAfter, WF, NS - 1>(q);
-          else
-            __builtin_amdgcn_s_waitcnt(vmcnt_imm(kDmaAfter));
-          qd_barrier();  // X(t+1) visible to every wave; its old stage free for the next DMA
+          for (int m = 0; m < MT; ++m) acc[m] = mfma16(xf[h][m], wf, acc[m]);
         }
+        qd_order();
+        dma_x((t + NS - 1) % NS, t + NS - 1);  // into the stage every wave finished reading in step t - 1
+        qd_order();
+        if (q == 3) fetch(j + DPF, wr[jj]);  // slot consumed
+        qd_order();
+        // X(t+1) landed: at most the instructions issued after its DMA pending -- the DMAs of
+        // steps t-NS+3 .. t and the W fetches of steps t-NS+2 .. t (those with s % 4 == 3); before
+        // step NS-2 its DMA came from the prologue (no fetch after it: the fetch-free count waits
+        // at least as long)
+        constexpr int kDmaAfter = (NS - 2) * PW;
+        if (t >= NS - 2)
+          qd_wait_steady<kDmaAfter, WF, NS - 1>(q);
+        else
+          __builtin_amdgcn_s_waitcnt(vmcnt_imm(kDmaAfter));
+        qd_barrier();  // X(t+1) visible to every wave; its old stage free for the next DMA
       }
     }
-  };
-  if (KH == 1 || kh == 0) steps(std::integral_constant<int, 0>{});
-  else steps(std::integral_constant<int, 1>{});
+  }
   wait_vmcnt0();  // the clamped tail DMAs land before the epilogue reuses the stages
   __syncthreads();
-  if constexpr (KH > 1) {  // acc = acc(even columns) + acc(odd columns), in that order for every M
-    float* kx = (float*)smem;  // [WN waves][NT][MT][64 lanes][4]
-    if (kh)
-#pragma unroll
-      for (int n = 0; n < NT; ++n)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) *(f32x4*)&kx[(((wn * NT + n) * MT + m) * 64 + lane) * 4] = acc[n][m];
-    __syncthreads();
-    if (!kh)
-#pragma unroll
-      for (int n = 0; n < NT; ++n)
-#pragma unroll
-        for (int m = 0; m < MT; ++m) acc[n][m] += *(const f32x4*)&kx[(((wn * NT + n) * MT + m) * 64 + lane) * 4];
-  }
 
-  // epilogue: acc[n][m][i] = C[row m*16 + 4g + i][col n0 + 16 (NT wn + n) + fr]; rows
-  // scaled by the deferred RMSNorm factor (one-tile RowScale), as k_dgemm.hip
-  if (rs.ssq && !kh) {
+  // epilogue: acc[m][i] = C[row m*16 + 4g + i][col n0 + 16 wn + fr]; rows scaled by the deferred
+  // RMSNorm factor (one-tile RowScale), as k_dgemm.hip
+  const int col = n0 + 16 * wn + fr;
+  if (rs.ssq) {
 #pragma unroll
     for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float r = rs_rinv(rs.ssq[min(m * 16 + 4 * g + i, M - 1)], rs);
-#pragma unroll
-        for (int n = 0; n < NT; ++n) acc[n][m][i] *= r;
-      }
+      for (int i = 0; i < 4; ++i) acc[m][i] *= rs_rinv(rs.ssq[min(m * 16 + 4 * g + i, M - 1)], rs);
   }
   if constexpr (EPI == MS_GEMV_EPI_SWIGLU) {
-    if constexpr (NT == 2) {  // the wave holds the gate (tile 0) and up (tile 1) rows of 16 features
-      if (kh) return;
-      const int f = (n0 >> 5) * 16 + wn * 16 + fr;
+    // waves 2p / 2p+1 hold the gate / up rows of the same 16 features (the fused matrix
+    // interleaves them by 16 rows); the stages are free after the loop's last barrier
+    float* xch = (float*)smem;
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+    for (int m = 0; m < MT; ++m) *(f32x4*)&xch[((wn * MT + m) * 64 + lane) * 4] = acc[m];
+    __syncthreads();
+    if (wn & 1) return;
+    const int f = (n0 >> 5) * 16 + (wn >> 1) * 16 + fr;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + 4 * g + i;
-          if (row < M && f < N / 2) {
-            const float gte = acc[0][m][i];
-            ((f16_t*)out)[(size_t)row * ldo + f] = f2h(gte / (1.0f + __expf(-gte)) * acc[1][m][i]);
-          }
-        }
-    } else {
-      // waves 2p / 2p+1 hold the gate / up rows of the same 16 features; a region of its own
-      // (the k-half exchange may still be read)
-      float* xch = (float*)(smem + (KH - 1) * XCH);
-      if (!kh)
+    for (int m = 0; m < MT; ++m) {
+      const f32x4 u = *(const f32x4*)&xch[(((wn + 1) * MT + m) * 64 + lane) * 4];
 #pragma unroll
-        for (int m = 0; m < MT; ++m) *(f32x4*)&xch[((wn * MT + m) * 64 + lane) * 4] = acc[0][m];
-      __syncthreads();
-      if (kh || (wn & 1)) return;
-      const int f = (n0 >> 5) * 16 + (wn >> 1) * 16 + fr;
-#pragma unroll
-      for (int m = 0; m < MT; ++m) {
-        const f32x4 u = *(const f32x4*)&xch[(((wn + 1) * MT + m) * 64 + lane) * 4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + 4 * g + i;
-          if (row < M && f < N / 2) {
-            const float gte = acc[0][m][i];
-            ((f16_t*)out)[(size_t)row * ldo + f] = f2h(gte / (1.0f + __expf(-gte)) * u[i]);
-          }
+      for (int i = 0; i < 4; ++i) {
+        const int row = m * 16 + 4 * g + i;
+        if (row < M && f < N / 2) {
+          const float gte = acc[m][i];
+          ((f16_t*)out)[(size_t)row * ldo + f] = f2h(gte / (1.0f + __expf(-gte)) * u[i]);
         }
       }
     }
   } else if constexpr (EPI == MS_GEMV_EPI_ARGMAX) {
-    if (kh) return;
-    // {max, id} of each row over each tile's 16 columns
+    // {max, id} of each row over this wave's 16 columns
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = n0 + 16 * (NT * wn + n) + fr;
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
+      for (int i = 0; i < 4; ++i) {
+        const int row = m * 16 + 4 * g + i;
+        float v = (col < N) ? acc[m][i] : -INFINITY;
+        if (!(v == v)) v = -INFINITY;
+        int idx = col;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + 4 * g + i;
-          float v = (col < N) ? acc[n][m][i] : -INFINITY;
-          if (!(v == v)) v = -INFINITY;
-          int idx = col;
-#pragma unroll
-          for (int o = 1; o < 16; o <<= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
-          if (fr == 0 && row < M)
-            ((float2*)out)[(size_t)row * ldo + (n0 >> 4) + NT * wn + n] = make_float2(v, __int_as_float(idx));
-        }
-    }
+        for (int o = 1; o < 16; o <<= 1) amax_merge_dev(v, idx, __shfl_xor(v, o, 64), __shfl_xor(idx, o, 64));
+        if (fr == 0 && row < M) ((float2*)out)[(size_t)row * ldo + (n0 >> 4) + wn] = make_float2(v, __int_as_float(idx));
+      }
   } else {
-    if (kh) return;
+    if (col >= N) return;
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = n0 + 16 * (NT * wn + n) + fr;
-      if (col >= N) continue;
+    for (int m = 0; m < MT; ++m)
 #pragma unroll
-      for (int m = 0; m < MT; ++m)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = m * 16 + 4 * g + i;
-          if (row < M) ((float*)out)[(size_t)row * ldo + col] = acc[n][m][i];
-        }
-    }
+      for (int i = 0; i < 4; ++i) {
+        const int row = m * 16 + 4 * g + i;
+        if (row < M) ((float*)out)[(size_t)row * ldo + col] = acc[m][i];
+      }
   }
 }
 
-static constexpr int kQdWn = 4;
-static constexpr int kQdRowAlign = 16 * kQdWn;  // region rows: whole blocks
+static constexpr int kQdRowAlign = 64;  // region rows: whole 64-row blocks
 
 // the row range [r0, r1) of region i of q
 static void qd_region(const QMat& q, int i, int N, int& r0, int& r1, const uint8_t*& base, int& type, int& rb) {
@@ -450,18 +387,13 @@ bool qdgemm_supported(int M, int N, int K, int S, int epi, const QMat& q) {
   return true;
 }
 
-// 4 waves x 16 rows, 64 rows per block.  (A k-half form -- 2 x 2 waves of two tiles each, the
-// wave groups splitting every step's MFMA columns -- measured no faster and lost its counted
-// waits whenever the compiler narrowed a half-used load: removed, r06 notes.)
-template <int MT, int QT, int WN, int DPF, int KH>
+template <int MT, int QT, int DPF>
 static void qdgemm_go(const f16_t* X, const QdSrc& src, void* out, int M, int Nr, int K, int S, int ldo,
                       int epi, const RowScale& rs, hipStream_t s) {
-  static_assert(KH == 1, "one-tile 4-wave form only");
-  constexpr int W_ = WN, NT_ = 1;
-  const dim3 grid(Nr / (16 * W_ * NT_), S), blk(64 * W_ * KH);
+  const dim3 grid(Nr / 64, S), blk(256);
   const int Ks = K / S;
   switch (epi) {
-#define QD(E_) MS_LAUNCH((qdgemm_kernel<MT, E_, W_, QT, DPF, KH, NT_>), grid, blk, 0, s, X, src, out, M, Nr, Ks, K, ldo, rs)
+#define QD(E_) MS_LAUNCH((qdgemm_kernel<MT, E_, QT, DPF>), grid, blk, 0, s, X, src, out, M, Nr, Ks, K, ldo, rs)
     case MS_GEMV_EPI_SWIGLU: QD(MS_GEMV_EPI_SWIGLU); break;
     case MS_GEMV_EPI_ARGMAX: QD(MS_GEMV_EPI_ARGMAX); break;
     default: QD(MS_GEMV_EPI_STORE_F32); break;
@@ -469,25 +401,29 @@ static void qdgemm_go(const f16_t* X, const QdSrc& src, void* out, int M, int Nr
   }
 }
 
-template <int QT, int DPF, int KH>
+template <int QT, int DPF>
 static void qdgemm_mt(const f16_t* X, const QdSrc& src, void* out, int M, int Nr, int K, int S, int ldo,
                       int epi, const RowScale& rs, hipStream_t s) {
-  {
-    const int mt = (M + 15) / 16;
-    if (mt <= 1) qdgemm_go<1, QT, kQdWn, DPF, KH>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
-    else if (mt <= 2) qdgemm_go<2, QT, kQdWn, DPF, KH>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
-    else if (mt <= 4) qdgemm_go<4, QT, kQdWn, DPF, KH>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
-    else if (mt <= 8) qdgemm_go<8, QT, kQdWn, DPF, KH>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
-    else if constexpr (KH == 1) qdgemm_go<16, QT, kQdWn, DPF, 1>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
-  }
+  const int mt = (M + 15) / 16;
+  if (mt <= 1) qdgemm_go<1, QT, DPF>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+  else if (mt <= 2) qdgemm_go<2, QT, DPF>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+  else if (mt <= 4) qdgemm_go<4, QT, DPF>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+  else if (mt <= 8) qdgemm_go<8, QT, DPF>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+  else qdgemm_go<16, QT, DPF>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
 }
 template <int QT>
 static void qdgemm_form(const f16_t* X, const QdSrc& src, void* out, int M, int Nr, int K, int S, int ldo,
                         int epi, const RowScale& rs, hipStream_t s) {
+  if constexpr (QT == kQdF16) {  // 32 VGPRs a ring slot: at most 3 in flight, preferring 2
+    const int nsb = K / S / 256;
+    if (nsb % 2 == 0) qdgemm_mt<QT, 2>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+    else qdgemm_mt<QT, 3>(X, src, out, M, Nr, K, S, ldo, epi, rs, s);
+    return;
+  }
   switch (qd_dpf(K / S / 256)) {
-    case 4: qdgemm_mt<QT, 4, 1>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
-    case 3: qdgemm_mt<QT, 3, 1>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
-    default: qdgemm_mt<QT, 2, 1>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
+    case 4: qdgemm_mt<QT, 4>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
+    case 3: qdgemm_mt<QT, 3>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
+    default: qdgemm_mt<QT, 2>(X, src, out, M, Nr, K, S, ldo, epi, rs, s); break;
   }
 }
 
@@ -506,6 +442,26 @@ void launch_qdgemm(const f16_t* X, const QMat& q, void* out, int M, int N, int K
             q.n > 2 ? q.row0_2 : N, q.row_bytes0};
   if (q.type0 == MS_QT_Q4_K) qdgemm_form<MS_QT_Q4_K>(X, src, out, M, N, K, S, ldo, epi, rs, s);
   else qdgemm_form<MS_QT_Q6_K>(X, src, out, M, N, K, S, ldo, epi, rs, s);
+}
+
+// the same kernel on fp16 rows W [N][K] (the engine's fp16 large-regime projections; tuning)
+bool qdgemm_f16_supported(int M, int N, int K, int S, int epi) {
+  const int nsb = S >= 1 && K % (256 * S) == 0 ? K / S / 256 : 0;
+  if (M < 1 || M > 256 || N % kQdRowAlign || !(nsb % 2 == 0 || nsb % 3 == 0) || nsb == 0) return false;
+  if (epi != MS_GEMV_EPI_STORE_F32 && epi != MS_GEMV_EPI_SWIGLU && epi != MS_GEMV_EPI_ARGMAX) return false;
+  return S == 1 || epi == MS_GEMV_EPI_STORE_F32;
+}
+void launch_qdgemm_f16(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+                       hipStream_t s, const RowScale* rs_in) {
+  if (!qdgemm_f16_supported(M, N, K, S, epi)) return;  // callers check
+  RowScale rs{};
+  if (rs_in && rs_in->ssq && epi != MS_GEMV_EPI_ARGMAX) {
+    if (rs_in->tiles != 1) return;
+    rs = *rs_in;
+  }
+  const uint8_t* b = (const uint8_t*)W;
+  QdSrc src{b, b, b, N, N, K * 2};
+  qdgemm_form<kQdF16>(X, src, out, M, N, K, S, ldo, epi, rs, s);
 }
 
 }  // namespace ms

@@ -232,6 +232,9 @@ struct QMat {
 bool qdgemm_supported(int M, int N, int K, int S, int epi, const QMat& q);
 void launch_qdgemm(const f16_t* X, const QMat& q, void* out, int M, int N, int K, int S, int ldo, int epi,
                    hipStream_t s, const RowScale* rs = nullptr);
+bool qdgemm_f16_supported(int M, int N, int K, int S, int epi);
+void launch_qdgemm_f16(const f16_t* X, const f16_t* W, void* out, int M, int N, int K, int S, int ldo, int epi,
+                       hipStream_t s, const RowScale* rs = nullptr);
 
 inline uint64_t smix_host(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;

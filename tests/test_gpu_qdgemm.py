@@ -131,3 +131,33 @@ def test_qdgemm_refuses_bad_shapes(lib, dev):
                             (8, 1024, 768, 3, L.MS_EPI_STORE_F32), (8, 1024, 768, 1, L.MS_EPI_STORE_F16)):
         assert lib.ms_op_qdgemm(X.data_ptr(), 12, pk.data_ptr(), out.data_ptr(), M, N, K, S, N, epi,
                                 _stream()) == L.MS_EINVAL
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("M", [1, 100, 128, 256])
+@pytest.mark.parametrize("N,K,S,epi", SHAPES)
+def test_qdgemm_fp16_rows(lib, dev, M, N, K, S, epi):
+    """The same kernel on fp16 rows (ggml type F16 = 1): fp32 outputs against float64, rows
+    independent of the launch's other rows."""
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + S + epi)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(torch.float16).to(dev)
+    X = torch.randn(256, K, generator=g).to(torch.float16).to(dev)
+    ncol = N // 2 if epi == L.MS_EPI_SWIGLU else (N // 16 if epi == L.MS_EPI_ARGMAX else N)
+    dt = torch.float16 if epi == L.MS_EPI_SWIGLU else torch.float32
+    width = ncol * (2 if epi == L.MS_EPI_ARGMAX else 1)
+    o = torch.zeros(S, M, width, dtype=dt, device=dev)
+    L.check(lib.ms_op_qdgemm(X.data_ptr(), 1, W.data_ptr(), o.data_ptr(), M, N, K, S, ncol, epi, _stream()))
+    full = torch.zeros(S, 256, width, dtype=dt, device=dev)
+    L.check(lib.ms_op_qdgemm(X.data_ptr(), 1, W.data_ptr(), full.data_ptr(), 256, N, K, S, ncol, epi, _stream()))
+    torch.cuda.synchronize()
+    assert torch.equal(o.cpu(), full[:, :M].cpu())
+    ref = X[:M].double() @ W.double().T
+    if epi == L.MS_EPI_STORE_F32:
+        ks = K // S
+        for s_ in range(S):
+            exp = X[:M].double()[:, s_ * ks:(s_ + 1) * ks] @ W.double()[:, s_ * ks:(s_ + 1) * ks].T
+            assert rel(o[s_].double(), exp) < 2e-6, s_
+    elif epi == L.MS_EPI_SWIGLU:
+        r = ref.view(M, N // 32, 2, 16)
+        exp = (torch.nn.functional.silu(r[:, :, 0]) * r[:, :, 1]).reshape(M, N // 2)
+        assert rel(o[0].double(), exp) < 4e-3

@@ -241,7 +241,11 @@ def bench_qdgemm(lib, ms=(64, 128, 256), only=None):
                 if lib.ms_op_dgemm(X.data_ptr(), ws16[0].data_ptr(), out.data_ptr(), M, N, K, S, lo, e, st) == 0:
                     t = timeit(lambda: lib.ms_op_dgemm(X.data_ptr(), nxt(ws16).data_ptr(), out.data_ptr(), M, N, K, S,
                                                        lo, e, st))
-                    line += f" f16 {t*1e3:6.1f}us |"
+                    line += f" f16 {t*1e3:6.1f}us"
+                if lib.ms_op_qdgemm(X.data_ptr(), 1, ws16[0].data_ptr(), out.data_ptr(), M, N, K, S, lo, e, st) == 0:
+                    t = timeit(lambda: lib.ms_op_qdgemm(X.data_ptr(), 1, nxt(ws16).data_ptr(), out.data_ptr(), M, N, K,
+                                                        S, lo, e, st))
+                    line += f" h {t*1e3:6.1f}us |"
             print(line, flush=True)
 
 def bench_camp(lib, M):
