@@ -64,6 +64,37 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
   const int wave_qlast = kvlen - qlen + min(q0 + 15, qlen - 1);  // keys after it: nothing to do
   const bool wave_live = q0 < qlen;
 
+  const int q_last = min(qb * QR + QR - 1, qlen - 1);
+  const int kv_end = kvlen - qlen + q_last + 1;  // keys visible to the block's last query
+  const int ntiles = (kv_end + 63) / 64;
+  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
+
+  // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
+  // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
+  auto page_of = [&](int t) { return kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t]; };
+  // (waves 0-3 load K, 4-7 V: J >> 4 = wave >> 2; the source array is picked once, in scalar
+  // registers -- a per-piece select reloaded the kernel argument by a vector load every tile)
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const bool dma_v = wave_u >= 4;
+  const f16_t* dma_src = dma_v ? kv.v : kv.k;
+  const int n_kv_heads = kv.n_kv_heads;
+  auto dma_tile = [&](int pid, int t, int buf) {
+    const f16_t* page = dma_src + ((size_t)pid * n_kv_heads + kvh) * kPage * kHeadDim;
+    const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
+    char* img = smem + buf * 32768 + (dma_v ? 16384 : 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int J = 4 * wave_u + i;
+      const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
+      const int srow = min(row, lim - 1);
+      const int sch = dma_v ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
+      dma16_opaque(page + srow * kHeadDim + sch * 8, img + 4 * (J & 15) * 256);
+    }
+  };
+  dma_tile(page_of(0), 0, 0);
+
+  // tile 0's K/V DMA is issued before the Q prologue's loads: the two round trips overlap
+  // (in-order vmcnt: the prologue's compiler-counted waits also cover these four pieces)
   // Q fragments live in LDS (each wave reads back only its own 16 rows, swizzled like K)
   char* qimg = smem + 2 * 32768;
   const int qrow_l = wave * 16 + r;
@@ -126,39 +157,11 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
     for (int i = 0; i < 8; ++i) o[hh][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const int q_last = min(qb * QR + QR - 1, qlen - 1);
-  const int kv_end = kvlen - qlen + q_last + 1;  // keys visible to the block's last query
-  const int ntiles = (kv_end + 63) / 64;
-  const int32_t* bt = kv.block_table + (size_t)slot * kv.max_pages;
-
-  // this wave's 4 DMA pieces of a tile: piece J = 4*wave + i covers rows 4(J % 16) ..+3 of
-  // K (J < 16) or V; lane -> row 4(J % 16) + lane / 16, LDS chunk lane % 16
-  auto page_of = [&](int t) { return kv.slot_major ? (int)(bt - kv.block_table) + t : bt[t]; };
-  // (waves 0-3 load K, 4-7 V: J >> 4 = wave >> 2; the source array is picked once, in scalar
-  // registers -- a per-piece select reloaded the kernel argument by a vector load every tile)
-  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  const bool dma_v = wave_u >= 4;
-  const f16_t* dma_src = dma_v ? kv.v : kv.k;
-  const int n_kv_heads = kv.n_kv_heads;
-  auto dma_tile = [&](int pid, int t, int buf) {
-    const f16_t* page = dma_src + ((size_t)pid * n_kv_heads + kvh) * kPage * kHeadDim;
-    const int lim = kvlen - t * 64;  // rows >= lim are past the sequence
-    char* img = smem + buf * 32768 + (dma_v ? 16384 : 0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int J = 4 * wave_u + i;
-      const int row = 4 * (J & 15) + (lane >> 4), c = lane & 15;
-      const int srow = min(row, lim - 1);
-      const int sch = dma_v ? (c ^ ((row & 7) << 1)) : (c ^ (row & 15));
-      dma16_opaque(page + srow * kHeadDim + sch * 8, img + 4 * (J & 15) * 256);
-    }
-  };
   // Lockstep: every wave runs QK, softmax and PV of tile t between two barriers.  A staggered
   // schedule (wave groups w < 4 and w >= 4, which share SIMDs, one phase apart so one wave's
   // QK MFMAs run beside the other's softmax) measured slower: 356 vs 295 us per layer at
   // configs[1] (two barriers and half-tile DMA waits per tile; profiles/r04/v5_*).
   // page ids run one tile ahead of the DMAs: tile t+1's DMA never waits on a table load
-  dma_tile(page_of(0), 0, 0);
   int pid_next = ntiles > 1 ? page_of(1) : 0;
   for (int t = 0; t < ntiles; ++t) {
     // tile t landed (its DMA and the next page id are the only global loads in flight), and
@@ -269,19 +272,35 @@ __global__ __launch_bounds__(512, 1) void attn_prefill_kernel(const f16_t* __res
         for (int hh = 0; hh < GB; ++hh) o[hh][dt] = mfma16(vt, pf[hh][kstep], o[hh][dt]);
       }
   }
-  if (wave_live && qi < qlen) {
+  // O / l through LDS, then stored as whole rows: a query's GB heads are one contiguous
+  // GB * 256-B run of its output row, written by consecutive lanes in 16-B pieces (per-lane 8-B
+  // stores at the row stride touched 16 rows per instruction).  Row stride GB * 256 + 16 B: the
+  // 16 rows of a ds_write_b64 land on distinct banks.
+  constexpr int OS = GB * 256 + 16;
+  __syncthreads();  // every wave is past its last tile: the tile buffers and the Q image are free
+  // lane indices recomputed here (v_mbcnt) rather than kept live across the tile loop, which
+  // holds all 256 registers
+  const int ln = __lane_id(), tid_e = wave_u * 64 + ln, row_e = wave_u * 16 + (ln & 15), g_e = ln >> 4;
+  if (wave_live) {
 #pragma unroll
     for (int hh = 0; hh < GB; ++hh) {
-      const float inv = 1.0f / l_run[hh];
-      f16_t* orow = out + (size_t)(qstart + qi) * (Hq * kHeadDim) + (h0 + hh) * kHeadDim;
+      const float inv = 1.0f / l_run[hh];  // rows past the sequence (l = 0) are never stored
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) {
         uint2 w;
         w.x = pack2h(o[hh][dt][0] * inv, o[hh][dt][1] * inv);
         w.y = pack2h(o[hh][dt][2] * inv, o[hh][dt][3] * inv);
-        *(uint2*)(orow + dt * 16 + 4 * g) = w;
+        *(uint2*)(smem + row_e * OS + hh * 256 + dt * 32 + 8 * g_e) = w;
       }
     }
+  }
+  __syncthreads();
+  constexpr int CPR = GB * 16;  // 16-B pieces per row
+  const int rows = min(QR, qlen - qb * QR);
+  f16_t* obase = out + (size_t)(qstart + qb * QR) * (Hq * kHeadDim) + h0 * kHeadDim;
+  for (int c = tid_e; c < rows * CPR; c += 512) {
+    const int row = c / CPR, col = c - row * CPR;
+    *(uint4*)(obase + (size_t)row * (Hq * kHeadDim) + col * 8) = *(const uint4*)(smem + row * OS + col * 16);
   }
 }
 
