@@ -235,6 +235,12 @@ struct ms_engine {
   // VALU; r06/v11_*) --, 2 every K-quant matrix, 0 none (the fp16 copies everywhere)
   int qlarge_min = 65;
   int qdgemm_mode = 1;
+  // engines of >= lm_gemm_min slots run the large-regime lm_head (its greedy partials) on the
+  // prefill GEMM's 128x128 tile (k_gemm.hip gemm_kernel, ~1000 blocks of 128 vocabulary rows)
+  // instead of the skinny GEMM: 169 vs 252 us at 128 rows, 276 vs 429 at 256
+  // (profiles/r06/v21_rows_dgemm_vs_gemm128.txt).  Per engine, so its arithmetic never changes
+  // with the rows of a step; MS_LM_GEMM_MIN (0 = never) for A/B.
+  int lm_gemm_min = 96;
   bool large(int) const { return large_engine && (!has_quant || cfg.max_batch >= qlarge_min); }
   // the K-quant skinny GEMM for this matrix (large regime)
   bool qd(const QSlot* q, int M, int N, int K, int S, int epi) const {
@@ -887,6 +893,7 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     E.large_engine = cfg->max_batch >= E.dgemm_min;
     if (const char* v = getenv("MS_QLARGE_MIN")) E.qlarge_min = atoi(v);
     if (const char* v = getenv("MS_QDGEMM")) E.qdgemm_mode = atoi(v);
+    if (const char* v = getenv("MS_LM_GEMM_MIN")) E.lm_gemm_min = atoi(v);
     // (the k-half block steps 128 k at a time: hidden sizes that are not a multiple of 128
     // keep the 4-wave block)
     E.dgemm_kh = cfg->max_batch <= 128 && E.H % 128 == 0 ? dgemm_kh_setting() : 1;
@@ -1544,6 +1551,8 @@ static void decode_body(ms_engine& E, int B, int32_t* d, const DecodeAttnArgs& d
     // 4-wave blocks always: a 2004-block grid keeps two per CU (k_dgemm.hip kh)
     if (E.qd(&E.lmq, B, E.V, E.H, 1, MS_GEMV_EPI_ARGMAX))
       launch_qdgemm(E.xb, E.lmq.m, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr);
+    else if (E.lm_gemm_min > 0 && E.cfg.max_batch >= E.lm_gemm_min && E.H % 64 == 0 && E.V % 16 == 0)
+      launch_gemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, tiles, MS_GEMV_EPI_ARGMAX, E.stream);
     else
       launch_dgemm(E.xb, E.lm_head, E.logits, B, E.V, E.H, 1, tiles, MS_GEMV_EPI_ARGMAX, E.stream, nullptr, 1,
                    B <= 128 && E.V % 128 == 0 ? E.dwn_lm : 4);
@@ -1988,15 +1997,19 @@ int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, in
                int32_t epi, void* stream) {
   return op_guard([&] {
     REQUIRE(A && W && out && M >= 1 && N >= 16 && K >= 64 && K % 64 == 0, MS_EINVAL, "bad gemm shape");
-    REQUIRE(epi >= 0 && epi <= 3 && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL, "bad epilogue");
+    REQUIRE(((epi >= 0 && epi <= 3) || epi == MS_EPI_ARGMAX) && (epi != MS_EPI_SWIGLU || N % 32 == 0), MS_EINVAL,
+            "bad epilogue");
     REQUIRE(epi != MS_EPI_ADD_F32 || (N % 4 == 0 && ldo % 4 == 0), MS_EINVAL,
             "residual gemm: N and ldo multiples of 4 (16-B x rows)");
+    // argmax: {max, id} float2 partials [M][ldo >= N / 16], the 128x128 tile, no row scale
+    REQUIRE(epi != MS_EPI_ARGMAX || (N % 16 == 0 && ldo >= N / 16), MS_EINVAL, "gemm argmax: N % 16, ldo >= N / 16");
     // the epilogues store 4 consecutive columns per lane (8 B fp16, 16 B fp32)
     REQUIRE(((uintptr_t)out & ((epi == MS_EPI_ADD_F32 || epi == MS_EPI_STORE_F32) ? 15 : 7)) == 0, MS_EINVAL,
             "gemm: out must be 16-B (fp32) / 8-B (fp16) aligned");
     REQUIRE(!g_op_rs.ssq || gemm_rs_tiles_ok(M, N, g_op_rs.tiles), MS_EINVAL,
             "gemm row scale: at most 24 tiles of statistics (kGemmRsTiles, both GEMM tiles)");
-    launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi, (hipStream_t)stream, &g_op_rs);
+    launch_gemm((const f16_t*)A, (const f16_t*)W, out, M, N, K, ldo, epi == MS_EPI_ARGMAX ? MS_GEMV_EPI_ARGMAX : epi,
+                (hipStream_t)stream, &g_op_rs);
   });
 }
 

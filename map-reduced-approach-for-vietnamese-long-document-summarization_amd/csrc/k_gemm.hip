@@ -236,6 +236,36 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(const f16_t* __restrict__ 
     if (fuse) gemm_resid_ssq_t<GBM, 1>(red, M, N, m0, n0, gr);
     return;
   }
+  if constexpr (EPI == MS_GEMV_EPI_ARGMAX) {
+    // greedy partials of the decode lm_head (MS_GEMV_EPI_ARGMAX's layout, finished by the decode
+    // tail / ms_op_argmax_partials): {max, id} of each row over each 16-column tile, ties to the
+    // lowest id, NaN never wins; no row scale (r > 0 keeps every row's order).  Lane (fr, fg)
+    // holds columns 4fg .. 4fg+3 of the tile; the 4 lane groups merge by two xor swaps.
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int row = m0 + wm * 64 + m * 16 + fr;
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int c0 = n0 + wn * 64 + n * 16;
+        float v = -INFINITY;
+        int idx = c0 + 4 * fg;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          float x = c0 + 4 * fg + j < N ? acc[m][n][j] : -INFINITY;
+          if (!(x == x)) x = -INFINITY;
+          if (x > v) { v = x; idx = c0 + 4 * fg + j; }
+        }
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+          const float v2 = __shfl_xor(v, o, 64);
+          const int i2 = __shfl_xor(idx, o, 64);
+          if (v2 > v || (v2 == v && i2 < idx)) { v = v2; idx = i2; }
+        }
+        if (fg == 0 && row < M && c0 < N) ((float2*)out)[(size_t)row * ldo + (c0 >> 4)] = make_float2(v, __int_as_float(idx));
+      }
+    }
+    return;
+  }
   gemm_rs_fold<GBM, kGemmRsTiles>(rs, rinv_s, rs_stage);
   {
     // acc[m][n][j] = C[row 16m + fr][col 16n + 4fg + j] of the wave's 64x64
@@ -822,6 +852,12 @@ int gemm_resid_tiles(int M, int N) {
 void launch_gemm(const f16_t* A, const f16_t* W, void* out, int M, int N, int K, int ldo, int epi,
                  hipStream_t s, const RowScale* rs_in, const GemmResid* gr_in) {
   if (M <= 0) return;
+  if (epi == MS_GEMV_EPI_ARGMAX) {  // the decode lm_head's greedy partials: the 128x128 tile only, no row scale
+    const int grid = ((M + GBM - 1) / GBM) * ((N + GBN - 1) / GBN);
+    MS_LAUNCH(gemm_kernel<MS_GEMV_EPI_ARGMAX>, dim3(grid), dim3(256), 0, s, A, W, out, M, N, K, ldo, RowScale{},
+              GemmResid{});
+    return;
+  }
   const bool big = gemm_big(M, N);
   RowScale rs{};
   if (rs_in && rs_in->ssq && epi != 1) {

@@ -361,9 +361,43 @@ def bench_gemm(lib, rs=False, variants=(1, 2), ascale=1.0, trunc=0, torch_ref=Fa
             print(f"torch   {name:5s} M={M} N={N} K={K}: {t:.3f} ms  {2*M*N*K/t/1e9:.0f} TFLOP/s", flush=True)
 
 
+def bench_rows(lib, ms=(128, 192, 256)):
+    """Decode projections at M = 128-256 rows: the decode skinny GEMM (k_dgemm.hip, its split-K
+    options) against the prefill GEMM's 128x128 tile (k_gemm.hip gemm_kernel, the small-M
+    dispatch) on the same operands, > 512 MB weight rotations (no MALL reuse)."""
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream().cuda_stream
+    for name, N, K, epi, splits in [("qkv", 5120, 3072, 0, (1, 2, 3)), ("o", 3072, 3072, 3, (1, 2, 4)),
+                                    ("gu", 16384, 3072, 2, (1,)), ("down", 3072, 8192, 3, (1, 2, 4, 8)),
+                                    ("lm_head", 128256, 3072, 0, (1,))]:
+        ws = [(torch.rand(N, K, device=dev) * 2 - 1).to(torch.float16)
+              for _ in range(max(2, -(-512 * 2**20 // (N * K * 2))))]
+        ldo = N // 2 if epi == 2 else N
+        i = [0]
+
+        def nxt():
+            i[0] += 1
+            return ws[i[0] % len(ws)]
+        for M in ms:
+            X = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.float16)
+            out = torch.zeros(8 * M * N, device=dev)
+            line = f"{name:8s} N={N:6d} K={K:5d} M={M:3d} {N*K*2/1e6:6.1f} MB |"
+            for S in splits:
+                e, lo = (epi, ldo) if S == 1 else (3, N)
+                if lib.ms_op_dgemm(X.data_ptr(), ws[0].data_ptr(), out.data_ptr(), M, N, K, S, lo, e, st) == 0:
+                    t = timeit(lambda: lib.ms_op_dgemm(X.data_ptr(), nxt().data_ptr(), out.data_ptr(), M, N, K, S,
+                                                       lo, e, st))
+                    line += f" dgemm S{S} {t*1e3:6.1f}us |"
+            L.check(lib.ms_set_gemm_variant(1))
+            t = timeit(lambda: lib.ms_op_gemm(X.data_ptr(), nxt().data_ptr(), out.data_ptr(), M, N, K, ldo, epi, st))
+            line += f" gemm128 {t*1e3:6.1f}us |"
+            L.check(lib.ms_set_gemm_variant(L.GEMM_DEFAULT))
+            print(line, flush=True)
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp", "qdgemm"])
+    ap.add_argument("what", choices=["gemv", "gemm", "split", "dgemm", "qgemv", "camp", "qdgemm", "rows"])
     ap.add_argument("--m", type=int, default=8)
     ap.add_argument("--ascale", type=float, default=1.0, help="gemm: scale of the uniform A entries")
     ap.add_argument("--trunc", type=int, default=0, help="gemm: clear this many low mantissa bits of A and W")
@@ -390,6 +424,8 @@ if __name__ == "__main__":
         bench_qgemv(lib, a.m)
     elif a.what == "camp":
         bench_camp(lib, a.m)
+    elif a.what == "rows":
+        bench_rows(lib, tuple(int(v) for v in a.ms.split(",")))
     elif a.what == "qdgemm":
         bench_qdgemm(lib, tuple(int(v) for v in a.ms.split(",")), a.only.split(",") if a.only else None)
     else:
