@@ -241,6 +241,15 @@ struct ms_engine {
   // (profiles/r06/v21_rows_dgemm_vs_gemm128.txt).  Per engine, so its arithmetic never changes
   // with the rows of a step; MS_LM_GEMM_MIN (0 = never) for A/B.
   int lm_gemm_min = 96;
+  // fp16 engines of >= qdf_min slots (16-row-tile launches of up to 256 rows) run their skinny
+  // GEMMs on k_qdgemm.hip's fp16-rows form (activations by LDS DMA three steps ahead) with
+  // QKV / down split 3 / 4 instead of 6 / 8: at 256 rows gate/up 57.3 -> 50.4 us, QKV 30.2 ->
+  // 22.6, down 43.3 -> 34.5, O 19.8 -> 19.2 (profiles/r06/v22_*).  Per engine (MS_QDF_MIN, 0 =
+  // never): below it the tested 24-128-slot arithmetic is unchanged.
+  int qdf_min = 192;
+  bool qdf(int M, int N, int K, int S, int epi) const {
+    return !has_quant && qdf_min > 0 && cfg.max_batch >= qdf_min && qdgemm_f16_supported(M, N, K, S, epi);
+  }
   bool large(int) const { return large_engine && (!has_quant || cfg.max_batch >= qlarge_min); }
   // the K-quant skinny GEMM for this matrix (large regime)
   bool qd(const QSlot* q, int M, int N, int K, int S, int epi) const {
@@ -480,6 +489,8 @@ struct ms_engine {
     if (large(M)) {  // skinny GEMM: the packed K-quant blocks, or the fp16 weights
       if (qd(q, M, N, K, Sl, MS_GEMV_EPI_STORE_F32))
         launch_qdgemm(X, q->m, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
+      else if (qdf(M, N, K, Sl, MS_GEMV_EPI_STORE_F32))
+        launch_qdgemm_f16(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs);
       else
         launch_dgemm(X, W, slabs, M, N, K, Sl, N, MS_GEMV_EPI_STORE_F32, stream, rs, 1,
                      M <= 128 && N % 128 == 0 ? dwn : 4);
@@ -573,6 +584,8 @@ struct ms_engine {
       prof_begin(K_GEMV);
       if (qd(&Q[QS_GU], B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU))
         launch_qdgemm(xb, Q[QS_GU].m, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn);
+      else if (qdf(B, 2 * F, H, 1, MS_GEMV_EPI_SWIGLU))
+        launch_qdgemm_f16(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn);
       else
         launch_dgemm(xb, Ly.wgu, hbuf, B, 2 * F, H, 1, F, MS_GEMV_EPI_SWIGLU, stream, &rs_ffn, dgemm_kh);
       prof_end(K_GEMV);
@@ -897,6 +910,11 @@ int ms_create(const ms_config* cfg, ms_engine** out) {
     // (the k-half block steps 128 k at a time: hidden sizes that are not a multiple of 128
     // keep the 4-wave block)
     E.dgemm_kh = cfg->max_batch <= 128 && E.H % 128 == 0 ? dgemm_kh_setting() : 1;
+    if (const char* v = getenv("MS_QDF_MIN")) E.qdf_min = atoi(v);
+    if (E.qdf_min > 0 && cfg->max_batch >= E.qdf_min) {  // splits measured at 256 rows (v22_*), any weights
+      E.dsplit_qkv = 3;
+      E.dsplit_down = 4;
+    }
     if (const char* v = getenv("MS_DSPLIT_QKV")) E.dsplit_qkv = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_O")) E.dsplit_o = atoi(v);
     if (const char* v = getenv("MS_DSPLIT_DOWN")) E.dsplit_down = atoi(v);

@@ -6,6 +6,9 @@ arithmetic is fixed at ms_create from max_batch (include/mapsum.h
   17-23 slots  GEMV, split-K O / down + residual_rmsnorm                  -> 20 slots here;
    >=24 slots  skinny GEMM (k_dgemm.hip), 8 KV pages per attention wave  -> 64 slots (the
                drop-in default, compat.py MAPSUM_MAX_BATCH) and 128 slots (configs[2]);
+   >=96 slots  the same, with the lm_head's greedy partials on the prefill GEMM's 128x128
+               tile                                                       -> 128 and 256 slots
+               (256: 16-row-tile skinny GEMMs, the configs[2] record's width);
 and K-quant engines (configs[4], Q4_K_M) keep the exact Q-GEMV at every size: <= 16 slots
 with the residual epilogue, above that in row groups of <= 64 rows with split-K O / down
 -> 8 and 128 slots here.  The reference hands the engine every chunk at once
@@ -43,8 +46,8 @@ from mapsum.engine import Engine  # noqa: E402
 HERE = os.path.dirname(os.path.abspath(__file__))
 # sharpq4km: the copy head on the Q4_K_M weights, quantised into K-quant
 # blocks (tests/golden/sharp_model.py q4km_overrides) -- the decisive greedy bar on K-quant weights
-RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(8, "q4km"), (128, "q4km")] + \
-    [(8, "sharpq4km"), (128, "sharpq4km")]
+RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(256, "sharp")] + \
+    [(8, "q4km"), (128, "q4km")] + [(8, "sharpq4km"), (128, "sharpq4km")]
 CASES = [(s, w, ci) for s, w in RUNS for ci in ((0, 3) if w in ("sharp", "sharpq4km") else (0, 5))]
 _CACHE = {}
 _OVERRIDES = {}
