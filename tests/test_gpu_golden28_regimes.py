@@ -46,7 +46,7 @@ from mapsum.engine import Engine  # noqa: E402
 HERE = os.path.dirname(os.path.abspath(__file__))
 # sharpq4km: the copy head on the Q4_K_M weights, quantised into K-quant
 # blocks (tests/golden/sharp_model.py q4km_overrides) -- the decisive greedy bar on K-quant weights
-RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(256, "sharp")] + \
+RUNS = [(s, w) for s in (20, 64, 128) for w in ("flat", "sharp")] + [(256, "flat"), (256, "sharp")] + \
     [(8, "q4km"), (128, "q4km")] + [(8, "sharpq4km"), (128, "sharpq4km")]
 CASES = [(s, w, ci) for s, w in RUNS for ci in ((0, 3) if w in ("sharp", "sharpq4km") else (0, 5))]
 _CACHE = {}
