@@ -87,9 +87,12 @@ typedef struct ms_config {
   int32_t max_batch;            /* sequences in flight (<= 1024).  Also fixes the
                                    engine's decode arithmetic (fp16 weights:
                                    1-16 residual-fused GEMV, 17-23 split GEMV +
-                                   residual_rmsnorm, >= 24 skinny GEMM; K-quant:
-                                   1-16 residual-fused Q-GEMV, >= 17 split
-                                   Q-GEMV + residual_rmsnorm); results
+                                   residual_rmsnorm, 24-95 skinny GEMM, 96-191
+                                   + the lm_head on the 128x128 GEMM tile,
+                                   >= 192 + the fp16-rows K-quant GEMM form;
+                                   K-quant: 1-16 residual-fused Q-GEMV, 17-64
+                                   split Q-GEMV + residual_rmsnorm, >= 65 the
+                                   K-quant skinny GEMM, lm_head tile from 96); results
                                    are batch-invariant inside one engine, not
                                    across these boundaries */
   int32_t max_ctx;              /* prompt + generated tokens per sequence     */
@@ -236,7 +239,9 @@ int ms_submit_forced(ms_engine* e, const int32_t* ids, int32_t n, const int32_t*
 #define MS_EPI_ARGMAX 5      /* decode GEMV only: out {max, id} float2 [M][ldo = N/16], one per
                                 16-column tile (ties -> lowest id; NaN never wins); finish the
                                 rows with ms_op_argmax_partials                          */
-/* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0 */
+/* prefill GEMM: out[M][N] (op) A[M][K] . W[N][K]^T ; K % 64 == 0.  MS_EPI_ARGMAX (the large
+   decode regime's lm_head): {max, id} float2 partials [M][ldo >= N/16] per 16-column tile on the
+   128x128 tile, no row scale, N % 16 == 0 */
 int ms_op_gemm(const void* A, const void* W, void* out, int32_t M, int32_t N, int32_t K,
                int32_t ldo, int32_t epilogue, void* stream);
 /* prefill O / down with the residual update fused (the engine's prefill layer): x fp32 [M][N] +=
