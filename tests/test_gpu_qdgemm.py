@@ -133,9 +133,15 @@ def test_qdgemm_refuses_bad_shapes(lib, dev):
                                 _stream()) == L.MS_EINVAL
 
 
+# the fp16-rows form as fp16 engines of >= 192 slots launch it (engine.cpp qdf): QKV split 3,
+# O and down split 4, gate/up SwiGLU
+F16_ENGINE_SHAPES = [(5120, 3072, 3, L.MS_EPI_STORE_F32), (3072, 3072, 4, L.MS_EPI_STORE_F32),
+                     (3072, 8192, 4, L.MS_EPI_STORE_F32)]
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("M", [1, 100, 128, 256])
-@pytest.mark.parametrize("N,K,S,epi", SHAPES)
+@pytest.mark.parametrize("N,K,S,epi", SHAPES + F16_ENGINE_SHAPES)
 def test_qdgemm_fp16_rows(lib, dev, M, N, K, S, epi):
     """The same kernel on fp16 rows (ggml type F16 = 1): fp32 outputs against float64, rows
     independent of the launch's other rows."""
